@@ -1,0 +1,263 @@
+"""Benchmark of the render hot path (BASELINE.json metric).
+
+One step = one frame: every rank renders its screen bands of the 1080p frame
+(rt_render_device, inputs resident in HBM), then the packed pixel bands are
+gathered to rank 0 over RCCL and re-interleaved into the frame.
+`value` = rays traced by all ranks (primary + shadow) / max-over-ranks time.
+
+    python bench.py [--gpus N --steps K --warmup W --config c3]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "real-time-opencl-raytracer_amd")
+for _p in (PKG, ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "Mrays/sec (primary+1 shadow) @1080p, 1M-tri SAH BVH; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # BASELINE.json configs[2] -- the metric's configuration
+    "c3": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, w=1920, h=1080, depth=1, flags=0,
+               desc="C3: 1M-tri value-noise heightfield (500x1000 cells x2, seed 0x5EED), 1920x1080, "
+                    "primary + 1 shadow ray, binned-SAH BVH"),
+    # configs[1]: ~70k-tri mesh, primary only
+    "c2": dict(scene="knot", nu=256, nv=137, w=1920, h=1080, depth=1, flags=1,
+               desc="C2: 70,144-tri torus knot, 1920x1080, primary rays only"),
+    # configs[3]: C3 scene at 4K (multi-GPU scaling curve)
+    "c4": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, w=3840, h=2160, depth=1, flags=0,
+               desc="C4: C3 scene at 3840x2160, primary + 1 shadow ray"),
+    # configs[4]: 10M tris (10 x C3 on a 5x2 grid), depth 3 (primary + 2 bounces, shadows)
+    "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, w=1920, h=1080, depth=3, flags=0,
+               desc="C5: 10M-tri merged scene (10 x C3 on a 5x2 grid), 1920x1080, 3 bounces with shadows"),
+}
+
+
+def make_scene(cfg, threads):
+    import rtamd
+    if cfg["scene"] == "heightfield":
+        mesh = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"])
+    elif cfg["scene"] == "knot":
+        mesh = rtamd.Mesh.torus_knot(cfg["nu"], cfg["nv"])
+    elif cfg["scene"] == "hf10":
+        tile = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"])
+        mesh = rtamd.Mesh()
+        mesh.append_grid(tile, 5, 2, 40.0, 100.0, 0.2)
+    else:
+        raise ValueError(cfg["scene"])
+    t0 = time.time()
+    bvh = mesh.build_bvh(8, threads)
+    return mesh, bvh, time.time() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import rtamd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = CONFIGS[args.config]
+    w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"]
+
+    host_threads = max(1, min(16, (os.cpu_count() or 1)) // max(1, world))
+    mesh, bvh, build_s = make_scene(cfg, host_threads)
+    scene = rtamd.Scene.from_mesh(mesh, bvh)
+    params = rtamd.params_to_array(mesh.camera_params(w, h))
+    r = rtamd.Renderer(local)
+    r.upload(scene)
+    r.set_params(params)
+
+    tiling = rtamd.rt_tiling(rank, world, args.band_rows, 0)
+    npx = rtamd.tiling_pixels(w, h, rank, world, args.band_rows)
+    nbands = (h + args.band_rows - 1) // args.band_rows
+    max_rows = ((nbands + world - 1) // world) * args.band_rows
+    cap = max_rows * w  # equal-size gather slots
+    out = torch.zeros(cap, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    gather = [torch.zeros(cap, dtype=torch.int32, device=dev) for _ in range(world)] if (world > 1 and rank == 0) \
+        else None
+    # at N = 1 the rank's buffer is the frame; at N > 1 rank 0 re-interleaves the gathered bands
+    frame = torch.zeros(h * w, dtype=torch.int32, device=dev) if (rank == 0 and world > 1) else None
+
+    # rays traced per frame by this rank (counted once with the aux planes)
+    d = max(depth, 1)
+    hits = torch.zeros(npx * d * 2, dtype=torch.int32, device=dev)
+    tt = torch.zeros(npx * d, dtype=torch.float32, device=dev)
+    rgb = torch.zeros(npx * 3, dtype=torch.float32, device=dev)
+    r.render_device(w, h, depth, flags, out.data_ptr(), tiling=tiling, stream=stream.cuda_stream,
+                    aux_ptrs=(hits.data_ptr(), tt.data_ptr(), rgb.data_ptr()))
+    torch.cuda.synchronize(dev)
+    hv = hits.view(npx, d, 2)
+    rays_local = int((hv[..., 0] != -2).sum().item()) + int((hv[..., 1] != -2).sum().item())
+    prim_local = int((hv[:, 0, 0] != -2).sum().item())
+    del hits, tt, rgb
+
+    # band -> frame re-interleave (rank 0): gathered slot r holds rank r's bands in order
+    def assemble():
+        if world == 1:
+            return
+        rows_per_rank = [rtamd.tiling_pixels(w, h, q, world, args.band_rows) // w for q in range(world)]
+        fv = frame.view(h, w)
+        for q in range(world):
+            src = gather[q].view(-1, w)
+            row = 0
+            for b in range(q, nbands, world):
+                n = min(args.band_rows, h - b * args.band_rows)
+                fv[b * args.band_rows:b * args.band_rows + n].copy_(src[row:row + n], non_blocking=True)
+                row += n
+            assert row == rows_per_rank[q]
+
+    def step():
+        r.render_device(w, h, depth, flags, out.data_ptr(), tiling=tiling, stream=stream.cuda_stream)
+        if world > 1:
+            dist.gather(out, gather_list=gather, dst=0)
+            if rank == 0:
+                assemble()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+
+    # per-launch kernel time from HIP events recorded on the launch stream
+    kms = []
+    for _ in range(max(3, min(args.steps, 20))):
+        r.render_device(w, h, depth, flags, out.data_ptr(), tiling=tiling, stream=stream.cuda_stream)
+        kms.append(r.last_kernel_ms())
+    kernel_ms_avg = float(np.mean(kms))
+
+    if world > 1:
+        t = torch.tensor([elapsed, float(rays_local), float(prim_local)], dtype=torch.float64, device=dev)
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax.item())
+        rays_total, prim_total = float(tsum[0].item()), float(tsum[1].item())
+        km = torch.tensor([kernel_ms_avg], dtype=torch.float64, device=dev)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kernel_ms_avg = float(km.item())
+    else:
+        rays_total, prim_total = float(rays_local), float(prim_local)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = rays_total * args.steps / elapsed / 1e6
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # CPU oracle sample: algorithmic bytes/ray (roofline) + CPU baseline
+    from oracle import oracle
+    cpu = None
+    bpr = None
+    budget = args.cpu_seconds if (world == 1 and not args.no_cpu_baseline) else min(args.cpu_seconds, 5.0)
+    ncores = min(16, os.cpu_count() or 1)
+    tprobe = time.perf_counter()
+    probe = oracle.render(scene, params, w, h, depth=depth, flags=flags, pixels=(0, (w * h) // 4093, 4093),
+                          nthreads=ncores, aux=False)
+    tprobe = time.perf_counter() - tprobe
+    per_px = tprobe / max(1, (w * h) // 4093)
+    npix_sample = int(min(w * h, max(1000, budget / max(per_px, 1e-9))))
+    stride = max(1, (w * h) // npix_sample)
+    npix_sample = (w * h) // stride
+    t0 = time.perf_counter()
+    samp = oracle.render(scene, params, w, h, depth=depth, flags=flags, pixels=(0, npix_sample, stride),
+                         nthreads=ncores, aux=False)
+    cpu_s = time.perf_counter() - t0
+    st = samp["stats"]
+    cpu_rays = sum(st[k]["rays"] for k in ("primary", "shadow", "secondary"))
+    kinds = [k for k in ("primary", "shadow", "secondary") if st[k]["rays"]]
+    tot_bytes = sum(80.0 * st[k]["inner"] + 16.0 * st[k]["leaf"] + 64.0 * st[k]["tris"] for k in kinds)
+    bpr = tot_bytes / max(1, cpu_rays)
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = {"value": cpu_rays / cpu_s / 1e6, "unit": "Mrays/s", "cores": ncores, "kind": "port",
+               "sample": f"oracle/rt_oracle.c on every {stride}th pixel of the same frame ({npix_sample} px, "
+                         f"{cpu_rays} rays, {cpu_s:.1f} s, {ncores} threads)"}
+
+    # algorithmic bytes per launch = rays this launch traces x bytes/ray + 4 B/pixel output
+    launch_rays = rays_total / max(1, world)
+    launch_bytes = launch_rays * bpr + 4.0 * (w * h) / max(1, world)
+    achieved = launch_bytes / (kernel_ms_avg * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": cfg["desc"], "config": args.config, "triangles": mesh.num_triangles,
+                   "bvh_nodes": int(bvh.nodes.shape[0]), "width": w, "height": h, "depth": depth,
+                   "shadow": not (flags & 1), "rays_per_frame": int(rays_total),
+                   "primary_rays_per_frame": int(prim_total), "parallelism": f"screen bands x{world} (RCCL gather)",
+                   "band_rows": args.band_rows, "bvh_build_s": round(build_s, 3)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_ray": round(bpr, 1), "kernel_ms": round(kernel_ms_avg, 4),
+                     "kernel": "rtk::render_kernel"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

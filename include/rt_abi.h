@@ -1,0 +1,158 @@
+/*
+ * rt_abi.h -- C ABI of the MI355X render path (the drop-in boundary).
+ *
+ * Replaces the reference's OpenCL host glue for kernel `raytracer_bvh`
+ * (x64/Release/volumeRender.cl:1043-1075).  Every entry point cites the
+ * reference code it stands in for.  Plain pointers and sizes only; no C++,
+ * torch or HIP types cross this boundary.
+ *
+ * Binary layouts are the reference's, byte for byte:
+ *   rt_bvh_node  == BVH_Node_            (BVH_Cuda.h:12-29)      48 B
+ *   rt_material  == Material             (Mesh.h:20-67)          176 B
+ *   rt_params    == Params / Params2     (RayTracer.cpp:115-161,
+ *                                         volumeRender.cl:320-330) 128 B
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rt_float4 { float x, y, z, w; } rt_float4;
+typedef struct rt_int4 { int32_t x, y, z, w; } rt_int4;
+
+/* BVH_Cuda.h:12-29 -- AABB{float4 min,max} + child/leaf words.
+ * Inner node: offset_left/right >= 0, offset_tris = -1, num_tris = 0.
+ * Leaf: offset_left = offset_right = -1, tris [offset_tris, +num_tris) of the
+ * reference-index array (values = 3 * triangle index, BVH_Cuda.h:90-93).
+ * Root = node 0; pre-order, left subtree first (BVH_Cuda.h:98-137). */
+typedef struct rt_bvh_node {
+    rt_float4 min, max;
+    int32_t offset_left, offset_right, offset_tris, num_tris;
+} rt_bvh_node;
+
+/* Mesh.h:20-67; the live kernel reads only .diffuse (volumeRender.cl:1381). */
+typedef struct rt_material {
+    rt_int4 technique;
+    rt_float4 emission, ambient, diffuse, specular, shininess;
+    rt_float4 reflective, reflectivity, transparent, transparency, glossiness;
+} rt_material;
+
+/* RayTracer.cpp:115-161 (w components = 1). */
+typedef struct rt_params {
+    rt_float4 a, b, c, campos, light_pos, light_color, scene_aabb_min, scene_aabb_max;
+} rt_params;
+
+#ifdef __cplusplus
+static_assert(sizeof(rt_bvh_node) == 48, "BVH_Node_ is 48 bytes");
+static_assert(sizeof(rt_material) == 176, "Material is 176 bytes");
+static_assert(sizeof(rt_params) == 128, "Params is 128 bytes");
+#endif
+
+/* Status codes (the reference used cl_int + CHECK_OPENCL_ERROR,
+ * RayTracer.cpp:338-344; the kernel itself has no error channel). */
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = -1,
+    RT_ERR_DEVICE = -2,      /* HIP runtime error; see rt_last_error() */
+    RT_ERR_NO_SCENE = -3,
+    RT_ERR_OUT_OF_MEMORY = -4,
+    RT_ERR_BAD_SCENE = -5    /* index out of range in the uploaded arrays */
+};
+
+/* rt_render flags */
+enum {
+    RT_FLAG_NO_SHADOW = 1u   /* config C2 "primary rays only": skip the any-hit shadow ray
+                                (volumeRender.cl:1437-1460); coefficient stays 1 */
+};
+
+#define RT_MAX_DEPTH 8       /* reference: RAY_TRACE_DEPTH 3 (volumeRender.cl:12) */
+
+typedef struct rt_ctx rt_ctx;
+
+/* Optional per-pixel side outputs (parity instrumentation).
+ * hits : int32 [P][depth][2] -- closest-hit id and shadow-hit id per bounce,
+ *        id = 3 * triangle index (volumeRender.cl:983), -1 = miss, -2 = not traced
+ * t    : float [P][depth]    -- closest-hit t per bounce (-1 = not traced)
+ * rgb  : float [P][3]        -- colour before the x255 pack (volumeRender.cl:1545) */
+typedef struct rt_aux {
+    int32_t* hits;
+    float* t;
+    float* rgb;
+} rt_aux;
+
+/* Screen sharding for multi-GPU.  Rows are cut into bands of
+ * band_rows rows; band b belongs to rank b % nranks.  A rank's output buffer
+ * holds only its bands, in increasing band order, each band_rows*w pixels
+ * (the last band may be short).  nranks = 1 renders the whole frame. */
+typedef struct rt_tiling {
+    int32_t rank, nranks, band_rows, reserved;
+} rt_tiling;
+
+/* Replaces setupCL's device/queue selection (RayTracer.cpp:2370-2433,
+ * CreateContext :2050, CreateCommandQueue :2097). */
+int rt_create(int device, rt_ctx** out);
+
+/* Replaces initRayTrace's clCreateBuffer(COPY_HOST_PTR) block
+ * (RayTracer.cpp:942-984) and initCLVolume2's argument setup (:1234-1261).
+ * Deep-copies the caller's arrays (caller keeps ownership) and builds the
+ * device-side layouts.  Arg numbers refer to raytracer_bvh (volumeRender.cl:1043):
+ *   verts/nv        arg 6  mesh_vertices        float4[nv]
+ *   idx/nidx        arg 7  mesh_indices         int[nidx]  (3 per triangle)
+ *   nodes/nn        arg 8  bvh_nodes            BVH_Node_[nn]   (arg 11 = nn)
+ *   refs/nref       arg 9  bvh_tris_indices     int[nref]        (arg 10 = nref)
+ *   normals/nnorm   arg 13 mesh_normals         float4[nnorm]
+ *   normal_idx      arg 14 mesh_normals_indices int[nidx]
+ *   mats/nmat       arg 15 mesh_materials       Material[nmat]
+ *   tri_to_mat      arg 16 tri -> material      int[nidx/3]
+ * Args 3/4 (brute-force triangle list, NULL/0 in the live path) and 12
+ * (debug `temp`) are dead in the reference and are not part of the ABI. */
+int rt_upload_scene(rt_ctx* ctx, const rt_float4* verts, int32_t nv, const int32_t* idx, int32_t nidx,
+                    const rt_bvh_node* nodes, int32_t nn, const int32_t* refs, int32_t nref,
+                    const rt_float4* normals, int32_t nnorm, const int32_t* normal_idx,
+                    const rt_material* mats, int32_t nmat, const int32_t* tri_to_mat);
+
+/* Replaces updateCamera's clEnqueueWriteBuffer of Params (RayTracer.cpp:671). */
+int rt_set_params(rt_ctx* ctx, const rt_params* params);
+
+/* Replaces raytrace_gpgpu (RayTracer.cpp:330-344): launch, finish, blocking
+ * readback of w*h packed pixels (b<<16 | g<<8 | r).  depth = number of bounces
+ * (reference: 3).  aux may be NULL.  Synchronous. */
+int rt_render(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr,
+              const rt_aux* aux);
+
+/* Device-resident variant for benchmarks and multi-GPU: renders this rank's
+ * bands (tiling may be NULL = whole frame) into device buffers d_out (and the
+ * optional device aux planes), enqueued on `stream` (a hipStream_t, NULL =
+ * the ctx stream).  Returns after enqueue; nothing is copied to the host. */
+int rt_render_device(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,
+                     const rt_tiling* tiling, uint32_t* d_out, const rt_aux* d_aux, void* stream);
+
+/* Number of pixels a rank owns under `tiling` (size of its output buffer). */
+int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* tiling);
+
+/* Kernel-side timing of the last render, from HIP events on the launch stream
+ * (ms); per-kernel breakdown for roofline accounting. */
+int rt_last_timing(rt_ctx* ctx, float* total_ms, float* traverse_ms);
+
+/* Device stack-overflow counter (reference: silent miss, volumeRender.cl:914). */
+int rt_overflow_count(rt_ctx* ctx, uint64_t* count);
+
+/* Releases all device memory (RayTraceData::~RayTraceData, RayTracer.cpp:208-228). */
+int rt_destroy(rt_ctx* ctx);
+
+/* Last error message for ctx (or the global one when ctx is NULL). */
+const char* rt_last_error(rt_ctx* ctx);
+
+/* ABI version for loaders. */
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_ABI_H */

@@ -1,0 +1,640 @@
+// rt_render.hip -- MI355X (gfx950) render path: device layouts, kernels, C ABI.
+//
+// Replaces the reference's per-pixel OpenCL kernel raytracer_bvh
+// (x64/Release/volumeRender.cl:1043-1547) and its host glue (RayTracer.cpp).
+// Results follow the reference kernel's arithmetic exactly; what
+// changes is how the data sits in HBM and how the traversal is scheduled:
+//
+//  * inner BVH nodes are re-laid out as 64-B records that carry BOTH child
+//    boxes plus the two child references (one 64-B fetch per inner visit
+//    instead of the reference's 16 B node word + 2 x 32 B child boxes in two
+//    dependent rounds, volumeRender.cl:836-867);
+//  * a child reference encodes leaf-ness and the leaf's triangle range, so a
+//    leaf never costs a node fetch;
+//  * triangle references are expanded into 48-B {v0, e1, e2, id} records in
+//    leaf order (the reference's 4-level ref -> index -> vertex gather,
+//    volumeRender.cl:965-974, becomes one contiguous 48-B read);
+//  * per-triangle shading data (3 vertices, 3 normals, albedo) is one 112-B
+//    record (volumeRender.cl:1306-1374 gathers from five arrays);
+//  * the 65-entry traversal stack (volumeRender.cl:636) lives in LDS for its
+//    first RTK_LDS_STACK entries, laid out [entry][lane] (bank-conflict free),
+//    the rest spills to a per-pixel global region; the top of stack stays in a
+//    register.  Stack semantics (including the overflow -> miss rule at 65)
+//    are the reference's, entry for entry;
+//  * one wave = one 8x8 pixel tile (the reference's work-group), 4 waves per
+//    block, blocks remapped so each XCD's L2 sees a contiguous screen strip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_abi.h"
+#include "rt_device_math.h"
+
+#ifndef RTK_LDS_STACK
+#define RTK_LDS_STACK 24
+#endif
+
+namespace rtk {
+
+constexpr int kStackSize = 65;                       // volumeRender.cl:636
+constexpr float kTmin = 0.001f;                      // volumeRender.cl:640
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kRefError = 0x7FFFFFFFu;          // popped -> traversal returns -1
+constexpr uint32_t kCntEscape = 31u;
+constexpr int kWavesPerBlock = 4;
+constexpr int kLdsStack = RTK_LDS_STACK;
+constexpr int kGlobalStack = 64 - kLdsStack;         // slots kLdsStack..63
+
+struct DevScene {
+    const float4* __restrict__ wnodes;   // [n_inner][4]
+    const float4* __restrict__ tris;     // [n_refs][3]
+    const float4* __restrict__ shade;    // [n_tris][7]
+    const int2* __restrict__ leaf_table; // escape leaves {offset, count}
+    uint32_t root;
+};
+
+struct Frame {
+    float3 a, b, c, campos, light_pos, smin, smax;
+    uint32_t w, h;
+    int32_t depth;
+    uint32_t flags;
+    int32_t rank, nranks, band_rows;
+    uint32_t local_rows;
+    uint32_t tiles_x, tiles_y, num_blocks;
+};
+
+struct Outputs {
+    uint32_t* out;
+    int32_t* hits;
+    float* t;
+    float* rgb;
+    uint32_t* gstack;            // [kGlobalStack][local_pixels]
+    unsigned long long* overflow;
+    uint64_t local_pixels;
+};
+
+__device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
+    uint32_t c = (ref >> 26) & 31u;
+    if (c == kCntEscape) {
+        int2 e = S.leaf_table[ref & 0x03FFFFFFu];
+        off = e.x;
+        cnt = e.y;
+    } else {
+        off = (int)(ref & 0x03FFFFFFu);
+        cnt = (int)c;
+    }
+}
+
+struct Stack {
+    uint32_t* lds;      // this lane's column: lds[i * 64]
+    uint32_t* glb;      // this pixel's column: glb[(i - kLdsStack) * gstride]
+    uint64_t gstride;
+    __device__ __forceinline__ uint32_t get(int i) const {
+        return i < kLdsStack ? lds[i * 64] : glb[(uint64_t)(i - kLdsStack) * gstride];
+    }
+    __device__ __forceinline__ void put(int i, uint32_t v) const {
+        if (i < kLdsStack) lds[i * 64] = v;
+        else glb[(uint64_t)(i - kLdsStack) * gstride] = v;
+    }
+};
+
+// traverse_bvh (volumeRender.cl:658-1010), reference visit order.
+template <bool CLOSEST>
+__device__ int traverse(const DevScene& S, const Ray& ray, float& tHit, const Stack& st, bool& overflow) {
+    uint32_t cur = S.root;
+    int sc = 1;            // stack_count; entry sc-1 is `cur`, entries 0..sc-2 are in `st`
+    int tri_index = -1;
+    const float ox = ray.ori.x, oy = ray.ori.y, oz = ray.ori.z;
+    const float dx = ray.dir.x, dy = ray.dir.y, dz = ray.dir.z;
+    while (true) {
+        if (cur & kLeafBit) {
+            int off, cnt;
+            leaf_range(S, cur, off, cnt);
+            const float4* tp = S.tris + (size_t)off * 3;
+            for (int i = 0; i < cnt; ++i) {
+                const float4 q0 = tp[3 * i + 0];
+                const float4 q1 = tp[3 * i + 1];
+                const float4 q2 = tp[3 * i + 2];
+                const float t = ray_tri(ray, F3{q0.x, q0.y, q0.z}, F3{q1.x, q1.y, q1.z}, F3{q2.x, q2.y, q2.z});
+                if (t < tHit && t > kTmin) {
+                    tHit = t;
+                    const int tri1 = __float_as_int(q0.w);
+                    if (!CLOSEST) return tri1;
+                    tri_index = tri1;
+                }
+            }
+            if (--sc == 0) break;
+            cur = st.get(sc - 1);
+            continue;
+        }
+        if (cur == kRefError) return -1;
+        const float4* np = S.wnodes + (size_t)cur * 4;
+        const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+        // ray_box (volumeRender.cl:612-624) on both children, IEEE division
+        float n0, f0, n1, f1;
+        {
+            const float ax = (q0.x - ox) / dx, ay = (q0.y - oy) / dy, az = (q0.z - oz) / dz;
+            const float bx = (q0.w - ox) / dx, by = (q1.x - oy) / dy, bz = (q1.y - oz) / dz;
+            n0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+            f0 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        }
+        {
+            const float ax = (q1.z - ox) / dx, ay = (q1.w - oy) / dy, az = (q2.x - oz) / dz;
+            const float bx = (q2.y - ox) / dx, by = (q2.z - oy) / dy, bz = (q2.w - oz) / dz;
+            n1 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+            f1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        }
+        const bool i0 = (n0 <= f0) && (f0 >= kTmin) && (n0 <= tHit);
+        const bool i1 = (n1 <= f1) && (f1 >= kTmin) && (n1 <= tHit);
+        const uint32_t r0 = __float_as_uint(q3.x), r1 = __float_as_uint(q3.y);
+        if (i0 && i1) {
+            uint32_t nearr = r0, farr = r1;
+            if (n0 > n1) { nearr = r1; farr = r0; }
+            if (sc >= kStackSize) {  // volumeRender.cl:914
+                overflow = true;
+                return -1;
+            }
+            st.put(sc - 1, farr);
+            cur = nearr;
+            ++sc;
+        } else if (i0) {
+            cur = r0;
+        } else if (i1) {
+            cur = r1;
+        } else {
+            if (--sc == 0) break;
+            cur = st.get(sc - 1);
+        }
+    }
+    return tri_index;
+}
+
+__global__ void __launch_bounds__(256) render_kernel(DevScene S, Frame F, Outputs O, int want_aux) {
+    __shared__ uint32_t s_stack[kWavesPerBlock][kLdsStack][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+
+    // XCD-aware block remap (bijective): blocks b, b+8, ... share an XCD; give
+    // each XCD a contiguous run of tiles.
+    const uint32_t nb = F.num_blocks, b = blockIdx.x;
+    const uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
+    const uint32_t tb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const uint32_t tx = tb % F.tiles_x, ty = tb / F.tiles_x;
+    const uint32_t x = tx * 16 + (wave & 1) * 8 + (lane & 7);
+    const uint32_t lr = ty * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (x >= F.w || lr >= F.local_rows) return;
+    uint32_t y = lr;
+    if (F.nranks > 1) {
+        const uint32_t band = lr / (uint32_t)F.band_rows, rib = lr % (uint32_t)F.band_rows;
+        y = (band * (uint32_t)F.nranks + (uint32_t)F.rank) * (uint32_t)F.band_rows + rib;
+    }
+    if (y >= F.h) return;
+    const uint64_t pix = (uint64_t)lr * F.w + x;
+
+    Stack st;
+    st.lds = &s_stack[wave][0][lane];
+    st.glb = O.gstack + pix;
+    st.gstride = O.local_pixels;
+    bool overflow = false;
+
+    const int depth = F.depth;
+    if (want_aux) {
+        for (int k = 0; k < depth; ++k) {
+            O.hits[(pix * depth + k) * 2 + 0] = -2;
+            O.hits[(pix * depth + k) * 2 + 1] = -2;
+            O.t[pix * depth + k] = -1.0f;
+        }
+    }
+
+    // volumeRender.cl:1169-1190
+    const float xf = (float)(((double)x - 0.5) / (double)(float)F.w);
+    const float yf = (float)(((double)y - 0.5) / (double)(float)F.h);
+    const F3 a = F3{F.a.x, F.a.y, F.a.z}, bb = F3{F.b.x, F.b.y, F.b.z}, c = F3{F.c.x, F.c.y, F.c.z};
+    const F3 campos = F3{F.campos.x, F.campos.y, F.campos.z};
+    const F3 light_pos = F3{F.light_pos.x, F.light_pos.y, F.light_pos.z};
+    const F3 t1 = c + a * xf;
+    const F3 t2 = bb * yf;
+    const F3 image_pos = t1 + t2;
+    Ray ray = ray_init(image_pos, image_pos - campos);
+    float tHit = 4294967296.0f;  // HitRecordInit: t = UINT_MAX
+    bool cont = ray_box_scene(F3{F.smin.x, F.smin.y, F.smin.z}, F3{F.smax.x, F.smax.y, F.smax.z}, ray.ori,
+                              ray.inv_dir);
+    F3 color = F3{0, 0, 0};
+    float shadow_sum = 0.0f;
+    int ray_depth = 0;
+    const bool do_shadow = !(F.flags & RT_FLAG_NO_SHADOW);
+    while (cont && ray_depth < depth) {
+        const int hit = traverse<true>(S, ray, tHit, st, overflow);
+        if (want_aux) {
+            O.hits[(pix * depth + ray_depth) * 2] = hit;
+            O.t[pix * depth + ray_depth] = tHit;
+        }
+        if (hit >= 0) {
+            const int kk = ray_depth;
+            ray_depth++;
+            const float4* sp = S.shade + (size_t)(hit / 3) * 7;
+            const float4 p0 = sp[0], p1 = sp[1], p2 = sp[2], m0 = sp[3], m1 = sp[4], m2 = sp[5], alb = sp[6];
+            const F3 vNew = ray.ori + ray.dir * (tHit - 0.001f);
+            const F3 normal = normalize(normal_at(vNew, xyz(p0), xyz(p1), xyz(p2), xyz(m0), xyz(m1), xyz(m2)));
+            const F3 l1 = normalize(light_pos - vNew);
+            const F3 v = normalize(ray.ori - vNew);
+            const F3 n = normalize(normal);
+            const F3 albedo = xyz(alb);
+            const float f0 = 40.0f * (1.0f / 255.0f);
+            F3 rez = cook_torrance_ggx(n, l1, v, albedo, f0, 0.5f) * 3.0f;
+            rez = rez + F3{0.3f, 0.3f, 0.3f} * albedo;
+            const F3 hitpoint = vNew;
+            const F3 L = normalize(light_pos - hitpoint);
+            float shadow_coef = 1.0f;
+            if (do_shadow) {
+                const Ray sray = ray_init(hitpoint + L * 0.001f, L);
+                float ts = 4294967296.0f;
+                const int sh = traverse<false>(S, sray, ts, st, overflow);
+                if (want_aux) O.hits[(pix * depth + kk) * 2 + 1] = sh;
+                if (sh >= 0 && ts > 0.025f) shadow_coef = 0.25f;
+            }
+            color = color + rez;
+            shadow_sum += shadow_coef;
+            const F3 refl = reflect(ray.dir, normal);
+            ray = ray_init(hitpoint + refl * 0.001f, refl);
+            tHit = 4294967296.0f;
+        } else {
+            cont = false;
+        }
+    }
+    if (ray_depth >= 1) {
+        color = color / (float)ray_depth;
+        shadow_sum /= (float)ray_depth;
+        color = color * shadow_sum;
+    } else {
+        color = F3{0, 0, 0};
+    }
+    if (want_aux) {
+        O.rgb[pix * 3 + 0] = color.x;
+        O.rgb[pix * 3 + 1] = color.y;
+        O.rgb[pix * 3 + 2] = color.z;
+    }
+    O.out[pix] = rgb_to_int(color.x * 255.0f, color.y * 255.0f, color.z * 255.0f);
+    if (overflow) atomicAdd(O.overflow, 1ull);
+}
+
+}  // namespace rtk
+
+// ============================================================================
+// Host side: context, upload/repack, launch.
+// ============================================================================
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float4* d_wnodes = nullptr;
+    float4* d_tris = nullptr;
+    float4* d_shade = nullptr;
+    int2* d_leaf = nullptr;
+    uint32_t root = 0;
+    bool have_scene = false;
+    bool have_params = false;
+    rt_params params{};
+    uint32_t* d_out = nullptr; size_t out_cap = 0;
+    int32_t* d_hits = nullptr; size_t hits_cap = 0;
+    float* d_t = nullptr; size_t t_cap = 0;
+    float* d_rgb = nullptr; size_t rgb_cap = 0;
+    uint32_t* d_gstack = nullptr; size_t gstack_cap = 0;   // in pixels
+    unsigned long long* d_overflow = nullptr;
+    float last_ms = 0.0f;
+    bool timing_valid = false;
+    std::string err;
+};
+
+static std::string g_err;
+
+static int set_err(rt_ctx* c, const std::string& m, int code) {
+    if (c) c->err = m; else g_err = m;
+    return code;
+}
+
+#define HIPC(ctx, expr)                                                                          \
+    do {                                                                                         \
+        hipError_t e__ = (expr);                                                                 \
+        if (e__ != hipSuccess)                                                                   \
+            return set_err(ctx, std::string(#expr) + ": " + hipGetErrorString(e__), RT_ERR_DEVICE); \
+    } while (0)
+
+template <class T>
+static int ensure(rt_ctx* c, T*& p, size_t& cap, size_t n) {
+    if (n <= cap && p) return RT_OK;
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    hipError_t e = hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess) { p = nullptr; return set_err(c, std::string("hipMalloc: ") + hipGetErrorString(e), RT_ERR_OUT_OF_MEMORY); }
+    cap = n;
+    return RT_OK;
+}
+
+static void free_scene(rt_ctx* c) {
+    if (c->d_wnodes) (void)hipFree(c->d_wnodes);
+    if (c->d_tris) (void)hipFree(c->d_tris);
+    if (c->d_shade) (void)hipFree(c->d_shade);
+    if (c->d_leaf) (void)hipFree(c->d_leaf);
+    c->d_wnodes = nullptr; c->d_tris = nullptr; c->d_shade = nullptr; c->d_leaf = nullptr;
+    c->have_scene = false;
+}
+
+extern "C" {
+
+int rt_abi_version(void) { return 1; }
+
+const char* rt_last_error(rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int rt_create(int device, rt_ctx** out) {
+    if (!out) return set_err(nullptr, "rt_create: out is NULL", RT_ERR_INVALID_ARG);
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return set_err(nullptr, "rt_create: no HIP device", RT_ERR_DEVICE);
+    if (device < 0 || device >= n) return set_err(nullptr, "rt_create: bad device index", RT_ERR_INVALID_ARG);
+    rt_ctx* c = new rt_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc((void**)&c->d_overflow, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_overflow, 0, sizeof(unsigned long long)) != hipSuccess) {
+        delete c;
+        return set_err(nullptr, "rt_create: HIP init failed", RT_ERR_DEVICE);
+    }
+    *out = c;
+    return RT_OK;
+}
+
+int rt_destroy(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_scene(c);
+    if (c->d_out) (void)hipFree(c->d_out);
+    if (c->d_hits) (void)hipFree(c->d_hits);
+    if (c->d_t) (void)hipFree(c->d_t);
+    if (c->d_rgb) (void)hipFree(c->d_rgb);
+    if (c->d_gstack) (void)hipFree(c->d_gstack);
+    if (c->d_overflow) (void)hipFree(c->d_overflow);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RT_OK;
+}
+
+int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t* idx, int32_t nidx,
+                    const rt_bvh_node* nodes, int32_t nn, const int32_t* refs, int32_t nref,
+                    const rt_float4* normals, int32_t nnorm, const int32_t* normal_idx, const rt_material* mats,
+                    int32_t nmat, const int32_t* tri_to_mat) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (!verts || nv <= 0 || !idx || nidx <= 0 || nidx % 3 || !nodes || nn <= 0 || !refs || nref < 0 || !normals ||
+        nnorm <= 0 || !normal_idx || !mats || nmat <= 0 || !tri_to_mat)
+        return set_err(c, "rt_upload_scene: missing or empty array", RT_ERR_INVALID_ARG);
+    const int32_t ntri = nidx / 3;
+    for (int32_t i = 0; i < nidx; ++i) {
+        if (idx[i] < 0 || idx[i] >= nv) return set_err(c, "mesh_indices out of range", RT_ERR_BAD_SCENE);
+        if (normal_idx[i] < 0 || normal_idx[i] >= nnorm) return set_err(c, "mesh_normals_indices out of range", RT_ERR_BAD_SCENE);
+    }
+    for (int32_t t = 0; t < ntri; ++t)
+        if (tri_to_mat[t] < 0 || tri_to_mat[t] >= nmat) return set_err(c, "tri_to_material out of range", RT_ERR_BAD_SCENE);
+    for (int32_t i = 0; i < nref; ++i)
+        if (refs[i] < 0 || refs[i] % 3 != 0 || refs[i] + 2 >= nidx)
+            return set_err(c, "bvh_tris_indices entry out of range", RT_ERR_BAD_SCENE);
+
+    // --- reference encoding of every node (traverse_bvh semantics, volumeRender.cl:829-856) ---
+    std::vector<int32_t> inner_id(nn, -1);
+    std::vector<int2> leaf_table;
+    std::vector<uint32_t> ref_of(nn, 0);
+    // inner ids in pre-order of reachability from the root; detect cycles (the
+    // reference would spin forever on some of them).
+    {
+        std::vector<uint8_t> state(nn, 0);  // 0 new, 1 on path, 2 done
+        std::vector<std::pair<int32_t, int>> stk;
+        int32_t next = 0;
+        stk.push_back({0, 0});
+        while (!stk.empty()) {
+            auto& top = stk.back();
+            const int32_t n = top.first;
+            const rt_bvh_node& nd = nodes[n];
+            if (top.second == 0) {
+                if (state[n] == 2) { stk.pop_back(); continue; }
+                if (state[n] == 1) return set_err(c, "BVH has a cycle", RT_ERR_BAD_SCENE);
+                state[n] = 1;
+                bool valid_inner = nd.offset_left >= 0 && nd.offset_right >= 0 && nd.offset_left < nn && nd.offset_right < nn;
+                if (nd.offset_left >= 0 && valid_inner) inner_id[n] = next++;
+            }
+            const bool is_inner = nd.offset_left >= 0 && inner_id[n] >= 0;
+            if (is_inner && top.second < 2) {
+                int32_t child = top.second == 0 ? nd.offset_left : nd.offset_right;
+                top.second++;
+                if (state[child] == 1) return set_err(c, "BVH has a cycle", RT_ERR_BAD_SCENE);
+                if (state[child] == 0) stk.push_back({child, 0});
+                continue;
+            }
+            state[n] = 2;
+            stk.pop_back();
+        }
+        for (int32_t n = 0; n < nn; ++n) {
+            const rt_bvh_node& nd = nodes[n];
+            if (nd.offset_left >= 0) {
+                ref_of[n] = inner_id[n] >= 0 ? (uint32_t)inner_id[n] : rtk::kRefError;
+            } else {
+                int32_t off = nd.offset_tris, cnt = nd.num_tris < 0 ? 0 : nd.num_tris;
+                if (cnt > 0 && (off < 0 || (int64_t)off + cnt > nref))
+                    return set_err(c, "leaf triangle range out of bounds", RT_ERR_BAD_SCENE);
+                if (cnt == 0) off = 0;
+                if (cnt < (int32_t)rtk::kCntEscape && off < (1 << 26)) {
+                    ref_of[n] = rtk::kLeafBit | ((uint32_t)cnt << 26) | (uint32_t)off;
+                } else {
+                    if (leaf_table.size() >= (1u << 26)) return set_err(c, "too many escape leaves", RT_ERR_BAD_SCENE);
+                    ref_of[n] = rtk::kLeafBit | (rtk::kCntEscape << 26) | (uint32_t)leaf_table.size();
+                    leaf_table.push_back(make_int2(off, cnt));
+                }
+            }
+        }
+        int32_t n_inner = next;
+        std::vector<float4> wn((size_t)std::max(n_inner, 1) * 4, make_float4(0, 0, 0, 0));
+        for (int32_t n = 0; n < nn; ++n) {
+            if (inner_id[n] < 0) continue;
+            const rt_bvh_node& L = nodes[nodes[n].offset_left];
+            const rt_bvh_node& R = nodes[nodes[n].offset_right];
+            float4* q = &wn[(size_t)inner_id[n] * 4];
+            q[0] = make_float4(L.min.x, L.min.y, L.min.z, L.max.x);
+            q[1] = make_float4(L.max.y, L.max.z, R.min.x, R.min.y);
+            q[2] = make_float4(R.min.z, R.max.x, R.max.y, R.max.z);
+            uint32_t r0 = ref_of[nodes[n].offset_left], r1 = ref_of[nodes[n].offset_right];
+            float f0, f1;
+            std::memcpy(&f0, &r0, 4);
+            std::memcpy(&f1, &r1, 4);
+            q[3] = make_float4(f0, f1, 0.0f, 0.0f);
+        }
+        // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974)
+        std::vector<float4> tr((size_t)std::max(nref, 1) * 3, make_float4(0, 0, 0, 0));
+        for (int32_t i = 0; i < nref; ++i) {
+            const int32_t tri1 = refs[i];
+            const rt_float4 v0 = verts[idx[tri1]], v1 = verts[idx[tri1 + 1]], v2 = verts[idx[tri1 + 2]];
+            float idf;
+            std::memcpy(&idf, &tri1, 4);
+            tr[(size_t)i * 3 + 0] = make_float4(v0.x, v0.y, v0.z, idf);
+            tr[(size_t)i * 3 + 1] = make_float4(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z, 0.0f);
+            tr[(size_t)i * 3 + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.0f);
+        }
+        // per-triangle shading records (volumeRender.cl:1306-1374)
+        std::vector<float4> sh((size_t)ntri * 7);
+        for (int32_t t = 0; t < ntri; ++t) {
+            float4* s = &sh[(size_t)t * 7];
+            for (int k = 0; k < 3; ++k) {
+                const rt_float4 v = verts[idx[3 * t + k]];
+                const rt_float4 n = normals[normal_idx[3 * t + k]];
+                s[k] = make_float4(v.x, v.y, v.z, 0.0f);
+                s[3 + k] = make_float4(n.x, n.y, n.z, 0.0f);
+            }
+            const rt_float4 d = mats[tri_to_mat[t]].diffuse;
+            s[6] = make_float4(d.x, d.y, d.z, 0.0f);
+        }
+        if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
+
+        HIPC(c, hipSetDevice(c->device));
+        free_scene(c);
+        HIPC(c, hipMalloc((void**)&c->d_wnodes, wn.size() * sizeof(float4)));
+        HIPC(c, hipMalloc((void**)&c->d_tris, tr.size() * sizeof(float4)));
+        HIPC(c, hipMalloc((void**)&c->d_shade, sh.size() * sizeof(float4)));
+        HIPC(c, hipMalloc((void**)&c->d_leaf, leaf_table.size() * sizeof(int2)));
+        HIPC(c, hipMemcpy(c->d_wnodes, wn.data(), wn.size() * sizeof(float4), hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_tris, tr.data(), tr.size() * sizeof(float4), hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_shade, sh.data(), sh.size() * sizeof(float4), hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
+        c->root = ref_of[0];
+        c->have_scene = true;
+    }
+    return RT_OK;
+}
+
+int rt_set_params(rt_ctx* c, const rt_params* p) {
+    if (!c || !p) return RT_ERR_INVALID_ARG;
+    c->params = *p;
+    c->have_params = true;
+    return RT_OK;
+}
+
+int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* t) {
+    if (!t || t->nranks <= 1) return (int64_t)w * h;
+    if (t->band_rows <= 0 || t->rank < 0 || t->rank >= t->nranks) return -1;
+    const int64_t nbands = ((int64_t)h + t->band_rows - 1) / t->band_rows;
+    int64_t rows = 0;
+    for (int64_t b = t->rank; b < nbands; b += t->nranks) rows += std::min<int64_t>(t->band_rows, (int64_t)h - b * t->band_rows);
+    return rows * w;
+}
+
+int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_tiling* tiling,
+                     uint32_t* d_out, const rt_aux* d_aux, void* stream) {
+    if (!c || !d_out || w == 0 || h == 0 || depth < 0 || depth > RT_MAX_DEPTH)
+        return set_err(c, "rt_render_device: invalid argument", RT_ERR_INVALID_ARG);
+    if (!c->have_scene) return set_err(c, "rt_render_device: no scene uploaded", RT_ERR_NO_SCENE);
+    if (!c->have_params) return set_err(c, "rt_render_device: no params set", RT_ERR_NO_SCENE);
+    rt_tiling whole{0, 1, 16, 0};
+    const rt_tiling* T = tiling ? tiling : &whole;
+    const int64_t npix = rt_tiling_pixels(w, h, T);
+    if (npix < 0) return set_err(c, "rt_render_device: bad tiling", RT_ERR_INVALID_ARG);
+    const bool aux = d_aux && d_aux->hits && d_aux->t && d_aux->rgb;
+    if (d_aux && !aux && (d_aux->hits || d_aux->t || d_aux->rgb))
+        return set_err(c, "rt_render_device: aux needs hits, t and rgb together", RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    if (npix == 0) return RT_OK;
+    int rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+
+    rtk::Frame F;
+    const rt_params& P = c->params;
+    F.a = make_float3(P.a.x, P.a.y, P.a.z);
+    F.b = make_float3(P.b.x, P.b.y, P.b.z);
+    F.c = make_float3(P.c.x, P.c.y, P.c.z);
+    F.campos = make_float3(P.campos.x, P.campos.y, P.campos.z);
+    F.light_pos = make_float3(P.light_pos.x, P.light_pos.y, P.light_pos.z);
+    F.smin = make_float3(P.scene_aabb_min.x, P.scene_aabb_min.y, P.scene_aabb_min.z);
+    F.smax = make_float3(P.scene_aabb_max.x, P.scene_aabb_max.y, P.scene_aabb_max.z);
+    F.w = w;
+    F.h = h;
+    F.depth = depth;
+    F.flags = flags;
+    F.rank = T->nranks > 1 ? T->rank : 0;
+    F.nranks = T->nranks > 1 ? T->nranks : 1;
+    F.band_rows = T->nranks > 1 ? T->band_rows : 16;
+    F.local_rows = (uint32_t)(npix / w);
+    F.tiles_x = (w + 15) / 16;
+    F.tiles_y = (F.local_rows + 15) / 16;
+    F.num_blocks = F.tiles_x * F.tiles_y;
+
+    rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root};
+    rtk::Outputs O;
+    O.out = d_out;
+    O.hits = aux ? d_aux->hits : nullptr;
+    O.t = aux ? d_aux->t : nullptr;
+    O.rgb = aux ? d_aux->rgb : nullptr;
+    O.gstack = c->d_gstack;
+    O.overflow = c->d_overflow;
+    O.local_pixels = (uint64_t)npix;
+
+    HIPC(c, hipEventRecord(c->ev0, s));
+    hipLaunchKernelGGL(rtk::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipEventRecord(c->ev1, s));
+    c->timing_valid = true;
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr,
+              const rt_aux* aux) {
+    if (!c || !out_bgr) return set_err(c, "rt_render: invalid argument", RT_ERR_INVALID_ARG);
+    const size_t npix = (size_t)w * h;
+    HIPC(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->d_out, c->out_cap, npix);
+    if (rc) return rc;
+    rt_aux dev{nullptr, nullptr, nullptr};
+    const bool want = aux && (aux->hits || aux->t || aux->rgb);
+    if (want) {
+        size_t d = (size_t)std::max(depth, 1);
+        if ((rc = ensure(c, c->d_hits, c->hits_cap, npix * d * 2))) return rc;
+        if ((rc = ensure(c, c->d_t, c->t_cap, npix * d))) return rc;
+        if ((rc = ensure(c, c->d_rgb, c->rgb_cap, npix * 3))) return rc;
+        dev = rt_aux{c->d_hits, c->d_t, c->d_rgb};
+    }
+    rc = rt_render_device(c, w, h, depth, flags, nullptr, c->d_out, want ? &dev : nullptr, c->stream);
+    if (rc) return rc;
+    HIPC(c, hipMemcpyAsync(out_bgr, c->d_out, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    if (want) {
+        if (aux->hits) HIPC(c, hipMemcpyAsync(aux->hits, c->d_hits, npix * depth * 2 * 4, hipMemcpyDeviceToHost, c->stream));
+        if (aux->t) HIPC(c, hipMemcpyAsync(aux->t, c->d_t, npix * depth * 4, hipMemcpyDeviceToHost, c->stream));
+        if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb, c->d_rgb, npix * 3 * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_last_timing(rt_ctx* c, float* total_ms, float* traverse_ms) {
+    if (!c || !total_ms) return RT_ERR_INVALID_ARG;
+    if (!c->timing_valid) return set_err(c, "rt_last_timing: nothing rendered", RT_ERR_NO_SCENE);
+    HIPC(c, hipEventSynchronize(c->ev1));
+    float ms = 0;
+    HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    *total_ms = ms;
+    if (traverse_ms) *traverse_ms = ms;
+    return RT_OK;
+}
+
+int rt_overflow_count(rt_ctx* c, uint64_t* count) {
+    if (!c || !count) return RT_ERR_INVALID_ARG;
+    unsigned long long v = 0;
+    HIPC(c, hipMemcpy(&v, c->d_overflow, sizeof v, hipMemcpyDeviceToHost));
+    *count = v;
+    return RT_OK;
+}
+
+}  // extern "C"

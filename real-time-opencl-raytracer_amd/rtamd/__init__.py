@@ -1,0 +1,381 @@
+"""rtamd -- Python host mirror of the MI355X render path (ctypes over librtamd.so).
+
+The reference drives its kernel from C++ (RayTracer.cpp: initRayTrace :858,
+initCLVolume2 :1234, updateCamera :609, raytrace_gpgpu :330).  This module is
+the same sequence over the C ABI in include/rt_abi.h and include/rt_host.h:
+
+    mesh  = Mesh.heightfield(500, 1000, 10.0, 0x5EED)     # Mesh::init
+    bvh   = mesh.build_bvh()                              # BVH2::setMesh + BVH_Cuda::build_from_bvh2
+    scene = Scene.from_mesh(mesh, bvh)                    # the kernel's array arguments
+    r     = Renderer(device=0); r.upload(scene)           # clCreateBuffer x9 + clSetKernelArg
+    r.set_params(mesh.camera_params(1920, 1080))          # updateCamera
+    img   = r.render(1920, 1080, depth=1)                 # raytrace_gpgpu
+
+There is no CPU fallback: if librtamd.so is missing or no GPU is present the
+render calls raise.  The CPU restatement under oracle/ is test infrastructure.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "librtamd.so")
+
+RT_FLAG_NO_SHADOW = 1
+RT_MAX_DEPTH = 8
+ERRORS = {0: "RT_OK", -1: "RT_ERR_INVALID_ARG", -2: "RT_ERR_DEVICE", -3: "RT_ERR_NO_SCENE",
+          -4: "RT_ERR_OUT_OF_MEMORY", -5: "RT_ERR_BAD_SCENE"}
+
+
+class RtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class rt_float4(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("w", C.c_float)]
+
+
+class rt_params(C.Structure):
+    _fields_ = [(n, rt_float4) for n in
+                ("a", "b", "c", "campos", "light_pos", "light_color", "scene_aabb_min", "scene_aabb_max")]
+
+
+class rt_aux(C.Structure):
+    _fields_ = [("hits", C.c_void_p), ("t", C.c_void_p), ("rgb", C.c_void_p)]
+
+
+class rt_tiling(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("nranks", C.c_int32), ("band_rows", C.c_int32), ("reserved", C.c_int32)]
+
+
+class rt_mesh_view(C.Structure):
+    _fields_ = [("vertices", C.c_void_p), ("num_vertices", C.c_int32),
+                ("indices", C.c_void_p), ("num_indices", C.c_int32),
+                ("normals", C.c_void_p), ("num_normals", C.c_int32),
+                ("normals_indices", C.c_void_p),
+                ("materials", C.c_void_p), ("num_materials", C.c_int32),
+                ("tri_to_material", C.c_void_p),
+                ("scene_min", C.c_float * 3), ("scene_max", C.c_float * 3)]
+
+
+class rt_bvh_view(C.Structure):
+    _fields_ = [("nodes", C.c_void_p), ("num_nodes", C.c_int32),
+                ("tri_indices", C.c_void_p), ("num_tri_indices", C.c_int32),
+                ("max_depth", C.c_int32), ("num_leaves", C.c_int32),
+                ("build_seconds", C.c_double)]
+
+
+# every symbol include/rt_abi.h and include/rt_host.h declare
+ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_device",
+               "rt_tiling_pixels", "rt_last_timing", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_abi_version"]
+HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
+                "rt_mesh_gen_cornell", "rt_mesh_gen_torus_knot", "rt_mesh_gen_heightfield", "rt_mesh_gen_random",
+                "rt_mesh_append_grid", "rt_bvh_build", "rt_bvh_view_get", "rt_bvh_destroy", "rt_bvh_save",
+                "rt_bvh_load", "rt_camera_params"]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load librtamd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtError(-2, f"{LIB_PATH} not built (run __graft_entry__.build() or make -C {PKG_ROOT})")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, u32, f32 = C.c_void_p, C.c_int32, C.c_uint32, C.c_float
+        sig = {
+            "rt_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+            "rt_upload_scene": (C.c_int, [vp, vp, i32, vp, i32, vp, i32, vp, i32, vp, i32, vp, vp, i32, vp]),
+            "rt_set_params": (C.c_int, [vp, C.POINTER(rt_params)]),
+            "rt_render": (C.c_int, [vp, u32, u32, i32, u32, vp, C.POINTER(rt_aux)]),
+            "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
+            "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
+            "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
+            "rt_overflow_count": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+            "rt_destroy": (C.c_int, [vp]),
+            "rt_last_error": (C.c_char_p, [vp]),
+            "rt_abi_version": (C.c_int, []),
+            "rt_mesh_create": (vp, []),
+            "rt_mesh_destroy": (None, [vp]),
+            "rt_mesh_view_get": (C.c_int, [vp, C.POINTER(rt_mesh_view)]),
+            "rt_mesh_set": (C.c_int, [vp, vp, i32, vp, i32, vp, i32, vp, vp, i32, vp]),
+            "rt_mesh_load_obj": (C.c_int, [vp, C.c_char_p]),
+            "rt_mesh_gen_cornell": (C.c_int, [vp]),
+            "rt_mesh_gen_torus_knot": (C.c_int, [vp, i32, i32]),
+            "rt_mesh_gen_heightfield": (C.c_int, [vp, i32, i32, f32, u32]),
+            "rt_mesh_gen_random": (C.c_int, [vp, i32, f32, f32, u32]),
+            "rt_mesh_append_grid": (C.c_int, [vp, vp, i32, i32, f32, f32, f32]),
+            "rt_bvh_build": (C.c_int, [vp, i32, i32, C.POINTER(vp)]),
+            "rt_bvh_view_get": (C.c_int, [vp, C.POINTER(rt_bvh_view)]),
+            "rt_bvh_destroy": (None, [vp]),
+            "rt_bvh_save": (C.c_int, [vp, vp, C.c_char_p]),
+            "rt_bvh_load": (C.c_int, [vp, C.c_char_p, C.POINTER(vp)]),
+            "rt_camera_params": (C.c_int, [vp, u32, u32, f32, f32, f32, vp, vp, C.POINTER(rt_params)]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _check(code: int, ctx=None):
+    if code != 0:
+        msg = lib().rt_last_error(ctx)
+        raise RtError(code, msg.decode() if msg else "")
+
+
+def params_to_array(p: rt_params) -> np.ndarray:
+    return np.frombuffer(bytes(p), dtype=np.float32).copy()
+
+
+def array_to_params(a: np.ndarray) -> rt_params:
+    a = np.ascontiguousarray(a, dtype=np.float32).reshape(32)
+    return rt_params.from_buffer_copy(a.tobytes())
+
+
+@dataclass
+class Scene:
+    """The raytracer_bvh array arguments (volumeRender.cl:1043-1075) as numpy arrays.
+
+    nodes: float32 (nn, 12) raw BVH_Node_ words (words 8..11 are int32 bits)
+    materials: float32 (nm, 44) raw Material words (words 0..3 are int32 bits)
+    """
+    vertices: np.ndarray
+    indices: np.ndarray
+    nodes: np.ndarray
+    tri_indices: np.ndarray
+    normals: np.ndarray
+    normals_indices: np.ndarray
+    materials: np.ndarray
+    tri_to_material: np.ndarray
+    scene_min: np.ndarray = field(default_factory=lambda: np.zeros(3, np.float32))
+    scene_max: np.ndarray = field(default_factory=lambda: np.zeros(3, np.float32))
+
+    @property
+    def num_triangles(self) -> int:
+        return int(self.indices.size // 3)
+
+    def nodes_int(self) -> np.ndarray:
+        return self.nodes.view(np.int32)
+
+    def arrays(self) -> dict:
+        return {k: getattr(self, k) for k in ("vertices", "indices", "nodes", "tri_indices", "normals",
+                                              "normals_indices", "materials", "tri_to_material",
+                                              "scene_min", "scene_max")}
+
+    @staticmethod
+    def from_arrays(d) -> "Scene":
+        def g(k, dt):
+            return np.ascontiguousarray(d[k], dtype=dt)
+        return Scene(g("vertices", np.float32).reshape(-1, 4), g("indices", np.int32).reshape(-1),
+                     g("nodes", np.float32).reshape(-1, 12), g("tri_indices", np.int32).reshape(-1),
+                     g("normals", np.float32).reshape(-1, 4), g("normals_indices", np.int32).reshape(-1),
+                     g("materials", np.float32).reshape(-1, 44), g("tri_to_material", np.int32).reshape(-1),
+                     g("scene_min", np.float32).reshape(3), g("scene_max", np.float32).reshape(3))
+
+    @staticmethod
+    def from_mesh(mesh: "Mesh", bvh: "Bvh") -> "Scene":
+        m = mesh.arrays()
+        return Scene(m["vertices"], m["indices"], bvh.nodes, bvh.tri_indices, m["normals"],
+                     m["normals_indices"], m["materials"], m["tri_to_material"], m["scene_min"], m["scene_max"])
+
+
+class Mesh:
+    """Owning wrapper of rtamd::Mesh (Mesh.h:69-101)."""
+
+    def __init__(self):
+        self._h = lib().rt_mesh_create()
+        if not self._h:
+            raise RtError(-4, "rt_mesh_create")
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rt_mesh_destroy(self._h)
+            self._h = None
+
+    @classmethod
+    def cornell(cls) -> "Mesh":
+        m = cls(); _check(lib().rt_mesh_gen_cornell(m._h)); return m
+
+    @classmethod
+    def torus_knot(cls, nu=256, nv=137) -> "Mesh":
+        m = cls(); _check(lib().rt_mesh_gen_torus_knot(m._h, nu, nv)); return m
+
+    @classmethod
+    def heightfield(cls, nx=500, nz=1000, amplitude=10.0, seed=0x5EED) -> "Mesh":
+        m = cls(); _check(lib().rt_mesh_gen_heightfield(m._h, nx, nz, amplitude, seed)); return m
+
+    @classmethod
+    def random(cls, ntris, extent=80.0, size=6.0, seed=1) -> "Mesh":
+        m = cls(); _check(lib().rt_mesh_gen_random(m._h, ntris, extent, size, seed)); return m
+
+    @classmethod
+    def load_obj(cls, path: str) -> "Mesh":
+        m = cls(); _check(lib().rt_mesh_load_obj(m._h, path.encode())); return m
+
+    @classmethod
+    def from_arrays(cls, vertices, indices, normals=None, normals_indices=None, materials=None,
+                    tri_to_material=None) -> "Mesh":
+        m = cls()
+        v = np.ascontiguousarray(vertices, np.float32).reshape(-1, 4)
+        i = np.ascontiguousarray(indices, np.int32).reshape(-1)
+        n = None if normals is None else np.ascontiguousarray(normals, np.float32).reshape(-1, 4)
+        ni = None if normals_indices is None else np.ascontiguousarray(normals_indices, np.int32).reshape(-1)
+        mt = None if materials is None else np.ascontiguousarray(materials, np.float32).reshape(-1, 44)
+        tm = None if tri_to_material is None else np.ascontiguousarray(tri_to_material, np.int32).reshape(-1)
+        _check(lib().rt_mesh_set(m._h, _ptr(v), v.shape[0], _ptr(i), i.size, _ptr(n), 0 if n is None else n.shape[0],
+                                 _ptr(ni), _ptr(mt), 0 if mt is None else mt.shape[0], _ptr(tm)))
+        return m
+
+    def append_grid(self, src: "Mesh", gx: int, gz: int, dx: float, dz: float, scale: float = 1.0):
+        _check(lib().rt_mesh_append_grid(self._h, src._h, gx, gz, dx, dz, scale))
+        return self
+
+    def arrays(self) -> dict:
+        v = rt_mesh_view()
+        _check(lib().rt_mesh_view_get(self._h, C.byref(v)))
+
+        def cp(p, n, dt, w):
+            if n == 0:
+                return np.zeros((0, w) if w > 1 else 0, dt)
+            buf = (C.c_char * (n * w * 4)).from_address(p)
+            a = np.frombuffer(buf, dtype=dt).copy()
+            return a.reshape(-1, w) if w > 1 else a
+        return {
+            "vertices": cp(v.vertices, v.num_vertices, np.float32, 4),
+            "indices": cp(v.indices, v.num_indices, np.int32, 1),
+            "normals": cp(v.normals, v.num_normals, np.float32, 4),
+            "normals_indices": cp(v.normals_indices, v.num_indices, np.int32, 1),
+            "materials": cp(v.materials, v.num_materials, np.float32, 44),
+            "tri_to_material": cp(v.tri_to_material, v.num_indices // 3, np.int32, 1),
+            "scene_min": np.array(list(v.scene_min), np.float32),
+            "scene_max": np.array(list(v.scene_max), np.float32),
+        }
+
+    @property
+    def num_triangles(self) -> int:
+        v = rt_mesh_view()
+        _check(lib().rt_mesh_view_get(self._h, C.byref(v)))
+        return v.num_indices // 3
+
+    def build_bvh(self, max_leaf: int = 8, threads: int = 0) -> "Bvh":
+        h = C.c_void_p()
+        _check(lib().rt_bvh_build(self._h, max_leaf, threads, C.byref(h)))
+        return Bvh(h)
+
+    def load_bvh(self, path: str) -> "Bvh":
+        h = C.c_void_p()
+        _check(lib().rt_bvh_load(self._h, path.encode(), C.byref(h)))
+        return Bvh(h)
+
+    def camera_params(self, w: int, h: int, radius: float = 200.0, extra_alpha: float = 0.0,
+                      extra_beta: float = 0.0, light_pos=None, light_color=None) -> rt_params:
+        p = rt_params()
+        lp = None if light_pos is None else np.asarray(light_pos, np.float32)
+        lc = None if light_color is None else np.asarray(light_color, np.float32)
+        _check(lib().rt_camera_params(self._h, w, h, radius, extra_alpha, extra_beta, _ptr(lp), _ptr(lc),
+                                      C.byref(p)))
+        return p
+
+
+class Bvh:
+    def __init__(self, handle):
+        self._h = handle
+        v = rt_bvh_view()
+        _check(lib().rt_bvh_view_get(self._h, C.byref(v)))
+        nb = v.num_nodes * 48
+        self.nodes = np.frombuffer((C.c_char * nb).from_address(v.nodes), np.float32).copy().reshape(-1, 12)
+        nr = v.num_tri_indices
+        self.tri_indices = (np.frombuffer((C.c_char * (nr * 4)).from_address(v.tri_indices), np.int32).copy()
+                            if nr else np.zeros(0, np.int32))
+        self.max_depth = v.max_depth
+        self.num_leaves = v.num_leaves
+        self.build_seconds = v.build_seconds
+
+    def save(self, mesh: Mesh, path: str):
+        _check(lib().rt_bvh_save(self._h, mesh._h, path.encode()))
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rt_bvh_destroy(self._h)
+            self._h = None
+
+
+class Renderer:
+    """One rt_ctx = one GPU (RayTraceData + command queue in the reference)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(lib().rt_create(device, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rt_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def upload(self, s: Scene):
+        self._scene_keepalive = s
+        _check(lib().rt_upload_scene(
+            self._h, _ptr(s.vertices), s.vertices.shape[0], _ptr(s.indices), s.indices.size,
+            _ptr(s.nodes), s.nodes.shape[0], _ptr(s.tri_indices), s.tri_indices.size,
+            _ptr(s.normals), s.normals.shape[0], _ptr(s.normals_indices), _ptr(s.materials), s.materials.shape[0],
+            _ptr(s.tri_to_material)), self._h)
+
+    def set_params(self, p):
+        if isinstance(p, np.ndarray):
+            p = array_to_params(p)
+        _check(lib().rt_set_params(self._h, C.byref(p)), self._h)
+
+    def render(self, w: int, h: int, depth: int = 3, flags: int = 0, aux: bool = False):
+        out = np.zeros(w * h, np.uint32)
+        if aux:
+            d = max(depth, 1)
+            hits = np.zeros((w * h, d, 2), np.int32)
+            t = np.zeros((w * h, d), np.float32)
+            rgb = np.zeros((w * h, 3), np.float32)
+            ax = rt_aux(_ptr(hits).value, _ptr(t).value, _ptr(rgb).value)
+            _check(lib().rt_render(self._h, w, h, depth, flags, _ptr(out), C.byref(ax)), self._h)
+            return {"out": out, "hits": hits[:, :depth], "t": t[:, :depth], "rgb": rgb}
+        _check(lib().rt_render(self._h, w, h, depth, flags, _ptr(out), None), self._h)
+        return out
+
+    def render_device(self, w, h, depth, flags, d_out_ptr: int, tiling: Optional[rt_tiling] = None,
+                      stream: int = 0, aux_ptrs=None):
+        ax = None if aux_ptrs is None else C.byref(rt_aux(*aux_ptrs))
+        _check(lib().rt_render_device(self._h, w, h, depth, flags, None if tiling is None else C.byref(tiling),
+                                      C.c_void_p(d_out_ptr), ax, C.c_void_p(stream or None)), self._h)
+
+    def last_kernel_ms(self) -> float:
+        t = C.c_float()
+        _check(lib().rt_last_timing(self._h, C.byref(t), None), self._h)
+        return t.value
+
+    def overflow_count(self) -> int:
+        v = C.c_uint64()
+        _check(lib().rt_overflow_count(self._h, C.byref(v)), self._h)
+        return v.value
+
+
+def tiling_pixels(w: int, h: int, rank: int, nranks: int, band_rows: int) -> int:
+    t = rt_tiling(rank, nranks, band_rows, 0)
+    return int(lib().rt_tiling_pixels(w, h, C.byref(t)))

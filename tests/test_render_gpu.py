@@ -1,0 +1,133 @@
+"""Parity of the HIP render path (through the C ABI) with the CPU oracle.
+
+Bar: hit ids bit-exact, closest-hit t and float RGB bit-exact
+(the north star allows 1e-4 on RGB; the S_strict semantics make both sides
+deterministic so the test demands identity and reports the 1e-4 check
+separately), packed pixels bit-exact.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+RGB_TOL = 1e-4  # north star tolerance on float RGB
+
+
+def _scene(d):
+    import rtamd
+    return rtamd.Scene.from_arrays(d)
+
+
+def _oracle(d, depth, flags=0, w=None, h=None, params=None):
+    from oracle import oracle
+    w = int(d["w"]) if w is None else w
+    h = int(d["h"]) if h is None else h
+    return oracle.render(d, d["params"] if params is None else params, w, h, depth=depth, flags=flags)
+
+
+def _compare(gpu, ref, label):
+    assert np.array_equal(gpu["hits"], ref["hits"]), f"{label}: hit ids differ at " \
+        f"{np.argwhere(gpu['hits'] != ref['hits'])[:5].tolist()}"
+    assert np.array_equal(gpu["t"].view(np.uint32), ref["t"].view(np.uint32)), f"{label}: t differs"
+    assert np.max(np.abs(gpu["rgb"] - ref["rgb"])) <= RGB_TOL, f"{label}: rgb beyond 1e-4"
+    assert np.array_equal(gpu["rgb"].view(np.uint32), ref["rgb"].view(np.uint32)), f"{label}: rgb not bitwise"
+    assert np.array_equal(gpu["out"], ref["out"]), f"{label}: packed pixels differ"
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_fixture_depth3(renderer, name):
+    d = load_golden(name)
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    gpu = renderer.render(w, h, depth=3, aux=True)
+    _compare(gpu, _oracle(d, 3), name)
+    plain = renderer.render(w, h, depth=3)
+    assert np.array_equal(plain, gpu["out"])
+
+
+@pytest.mark.parametrize("name", ["cornell12", "knot16k", "hf40k", "rand2k"])
+@pytest.mark.parametrize("depth,flags", [(1, 0), (1, 1), (2, 0), (0, 0)])
+def test_depth_and_flags(renderer, name, depth, flags):
+    d = load_golden(name)
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    gpu = renderer.render(w, h, depth=depth, flags=flags, aux=True)
+    ref = _oracle(d, depth, flags)
+    _compare(gpu, ref, f"{name} depth={depth} flags={flags}")
+
+
+def test_odd_sizes(renderer):
+    d = load_golden("knot16k")
+    import rtamd
+    renderer.upload(_scene(d))
+    for (w, h) in [(1, 1), (17, 9), (123, 77)]:
+        m = rtamd.Mesh.torus_knot(128, 64)
+        p = rtamd.params_to_array(m.camera_params(w, h))
+        renderer.set_params(p)
+        gpu = renderer.render(w, h, depth=3, aux=True)
+        _compare(gpu, _oracle(d, 3, w=w, h=h, params=p), f"{w}x{h}")
+
+
+def test_overflow_counter(renderer):
+    d = load_golden("overflow_comb")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    before = renderer.overflow_count()
+    gpu = renderer.render(int(d["w"]), int(d["h"]), depth=3, aux=True)
+    ref = _oracle(d, 3)
+    _compare(gpu, ref, "overflow_comb")
+    assert ref["stats"]["stack_overflow"] > 0
+    assert renderer.overflow_count() > before
+
+
+@pytest.mark.parametrize("nranks,band_rows", [(2, 16), (3, 8), (8, 16)])
+def test_band_tiling_reassembles(renderer, nranks, band_rows):
+    """Each rank's bands (rt_tiling) re-interleave to the whole frame."""
+    import rtamd
+    import torch
+    d = load_golden("hf40k")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"]) - 8  # a short last band
+    full = renderer.render(w, h, depth=1)
+    img = np.zeros((h, w), np.uint32)
+    nbands = (h + band_rows - 1) // band_rows
+    for rank in range(nranks):
+        npx = rtamd.tiling_pixels(w, h, rank, nranks, band_rows)
+        buf = torch.zeros(max(npx, 1), dtype=torch.int32, device="cuda")
+        t = rtamd.rt_tiling(rank, nranks, band_rows, 0)
+        renderer.render_device(w, h, 1, 0, buf.data_ptr(), tiling=t, stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        local = buf.cpu().numpy().view(np.uint32)[:npx].reshape(-1, w)
+        row = 0
+        for b in range(rank, nbands, nranks):
+            n = min(band_rows, h - b * band_rows)
+            img[b * band_rows:b * band_rows + n] = local[row:row + n]
+            row += n
+    assert np.array_equal(img.reshape(-1), full)
+
+
+def test_errors(renderer):
+    import rtamd
+    r = rtamd.Renderer(0)
+    with pytest.raises(rtamd.RtError):
+        r.render(16, 16, depth=1)  # no scene
+    d = load_golden("cornell12")
+    s = _scene(d)
+    bad = rtamd.Scene.from_arrays(s.arrays())
+    bad.indices = bad.indices.copy()
+    bad.indices[0] = 10 ** 6
+    with pytest.raises(rtamd.RtError) as e:
+        r.upload(bad)
+    assert e.value.code == -5
+    r.upload(s)
+    with pytest.raises(rtamd.RtError):
+        r.render(16, 16, depth=1)  # no params
+    r.set_params(d["params"])
+    with pytest.raises(rtamd.RtError):
+        r.render(16, 16, depth=99)
+    r.close()
