@@ -26,20 +26,22 @@ for _p in (PKG, ROOT):
 
 METRIC = "Mrays/sec (primary+1 shadow) @1080p, 1M-tri SAH BVH; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# C3 terrain extent: fills the default camera's 1080p view (Camera.cpp:6-19)
+HF_EXT = (-150.0, 650.0, -150.0, 650.0)
 
 CONFIGS = {
     # BASELINE.json configs[2] -- the metric's configuration
-    "c3": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, w=1920, h=1080, depth=1, flags=0,
+    "c3": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=HF_EXT, w=1920, h=1080, depth=1, flags=0,
                desc="C3: 1M-tri value-noise heightfield (500x1000 cells x2, seed 0x5EED), 1920x1080, "
                     "primary + 1 shadow ray, binned-SAH BVH"),
     # configs[1]: ~70k-tri mesh, primary only
     "c2": dict(scene="knot", nu=256, nv=137, w=1920, h=1080, depth=1, flags=1,
                desc="C2: 70,144-tri torus knot, 1920x1080, primary rays only"),
     # configs[3]: C3 scene at 4K (multi-GPU scaling curve)
-    "c4": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, w=3840, h=2160, depth=1, flags=0,
+    "c4": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=HF_EXT, w=3840, h=2160, depth=1, flags=0,
                desc="C4: C3 scene at 3840x2160, primary + 1 shadow ray"),
     # configs[4]: 10M tris (10 x C3 on a 5x2 grid), depth 3 (primary + 2 bounces, shadows)
-    "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, w=1920, h=1080, depth=3, flags=0,
+    "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920, h=1080, depth=3, flags=0,
                desc="C5: 10M-tri merged scene (10 x C3 on a 5x2 grid), 1920x1080, 3 bounces with shadows"),
 }
 
@@ -47,13 +49,13 @@ CONFIGS = {
 def make_scene(cfg, threads):
     import rtamd
     if cfg["scene"] == "heightfield":
-        mesh = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"])
+        mesh = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"], cfg["ext"])
     elif cfg["scene"] == "knot":
         mesh = rtamd.Mesh.torus_knot(cfg["nu"], cfg["nv"])
     elif cfg["scene"] == "hf10":
-        tile = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"])
+        tile = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"], cfg["ext"])
         mesh = rtamd.Mesh()
-        mesh.append_grid(tile, 5, 2, 40.0, 100.0, 0.2)
+        mesh.append_grid(tile, 5, 2, 160.0, 400.0, 1.0)
     else:
         raise ValueError(cfg["scene"])
     t0 = time.time()

@@ -60,7 +60,9 @@ int rt_mesh_load_obj(rt_mesh* m, const char* path);
  * orbit camera (radius 200 around the origin). */
 int rt_mesh_gen_cornell(rt_mesh* m);                                    /* C1: 12 triangles */
 int rt_mesh_gen_torus_knot(rt_mesh* m, int32_t nu, int32_t nv);          /* C2: 2*nu*nv tris */
-int rt_mesh_gen_heightfield(rt_mesh* m, int32_t nx, int32_t nz, float amplitude, uint32_t seed); /* C3 */
+/* C3: value-noise heightfield over [x0,x1] x [z0,z1], 2*nx*nz triangles */
+int rt_mesh_gen_heightfield(rt_mesh* m, int32_t nx, int32_t nz, float amplitude, uint32_t seed, float x0, float x1,
+                            float z0, float z1);
 int rt_mesh_gen_random(rt_mesh* m, int32_t ntris, float extent, float size, uint32_t seed);
 /* Append `src` translated on a gx x gz grid with spacing (dx, dz) (C5 merge). */
 int rt_mesh_append_grid(rt_mesh* dst, const rt_mesh* src, int32_t gx, int32_t gz, float dx, float dz,

@@ -78,9 +78,10 @@ int rt_mesh_gen_torus_knot(rt_mesh* mh, int32_t nu, int32_t nv) {
     rtamd::gen_torus_knot(mh->m, nu, nv);
     return RT_OK;
 }
-int rt_mesh_gen_heightfield(rt_mesh* mh, int32_t nx, int32_t nz, float amplitude, uint32_t seed) {
-    if (!mh || nx < 1 || nz < 1) return RT_ERR_INVALID_ARG;
-    rtamd::gen_heightfield(mh->m, nx, nz, amplitude, seed);
+int rt_mesh_gen_heightfield(rt_mesh* mh, int32_t nx, int32_t nz, float amplitude, uint32_t seed, float x0, float x1,
+                            float z0, float z1) {
+    if (!mh || nx < 1 || nz < 1 || !(x1 > x0) || !(z1 > z0)) return RT_ERR_INVALID_ARG;
+    rtamd::gen_heightfield(mh->m, nx, nz, amplitude, seed, x0, x1, z0, z1);
     return RT_OK;
 }
 int rt_mesh_gen_random(rt_mesh* mh, int32_t ntris, float extent, float size, uint32_t seed) {

@@ -226,7 +226,7 @@ void gen_torus_knot(Mesh& m, int nu, int nv) {
     m.update_bounds();
 }
 
-// ---- C3: value-noise heightfield, nx*nz cells, 2 tris per cell, over [-100,100]^2 ----
+// ---- C3: value-noise heightfield, nx*nz cells, 2 tris per cell, over [x0,x1] x [z0,z1] ----
 static inline uint32_t hash32(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
     return x;
@@ -254,11 +254,11 @@ static double fbm(double x, double y, uint32_t seed) {
     return s / norm;
 }
 
-void gen_heightfield(Mesh& m, int nx, int nz, float amplitude, uint32_t seed) {
+void gen_heightfield(Mesh& m, int nx, int nz, float amplitude, uint32_t seed, float x0, float x1, float z0, float z1) {
     m = Mesh();
     m.materials.push_back(diffuse_material(0.35f, 0.6f, 0.3f));
     m.materials.push_back(diffuse_material(0.6f, 0.5f, 0.4f));
-    const double X0 = -100, X1 = 100, Z0 = -100, Z1 = 100;
+    const double X0 = x0, X1 = x1, Z0 = z0, Z1 = z1;
     const int vx = nx + 1, vz = nz + 1;
     auto height = [&](double x, double z) { return amplitude * fbm(x * 0.04, z * 0.04, seed) - 20.0; };
     m.vertices.resize((size_t)vx * vz);

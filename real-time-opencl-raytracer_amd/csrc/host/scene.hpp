@@ -43,7 +43,8 @@ rt_material diffuse_material(float r, float g, float b);
 int load_obj(const std::string& path, Mesh& m, std::string& err);
 void gen_cornell(Mesh& m);
 void gen_torus_knot(Mesh& m, int nu, int nv);
-void gen_heightfield(Mesh& m, int nx, int nz, float amplitude, uint32_t seed);
+void gen_heightfield(Mesh& m, int nx, int nz, float amplitude, uint32_t seed, float x0, float x1, float z0,
+                     float z1);
 void gen_random(Mesh& m, int ntris, float extent, float size, uint32_t seed);
 void append_grid(Mesh& dst, const Mesh& src, int gx, int gz, float dx, float dz, float scale);
 

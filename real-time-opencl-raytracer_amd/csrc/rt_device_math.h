@@ -4,11 +4,23 @@
 // source order, OpenCL builtins as ROCm device-libs define them, correctly
 // rounded '/' and sqrt, rsqrt and pow(x,5) in binary64).  This translation
 // unit is compiled with -ffp-contract=off: every fma below is explicit.
-#pragma once
-
+//
+// Included once per math mode (rt_render.hip): RTK_NS names the namespace and
+// RTK_HWMATH selects the two substituted functions:
+//   RTK_HWMATH = 0  rsqrt(x) = (float)(1/sqrt((double)x)), pow(x,5) in binary64
+//                   (S_strict: reproducible on any IEEE host -> the CPU oracle)
+//   RTK_HWMATH = 1  rsqrt = __ocml_rsqrt_f32 (v_rsq_f32), pow = __ocml_pow_f32,
+//                   i.e. what the reference kernel links on gfx950 (S_hw).
 #include <hip/hip_runtime.h>
 
-namespace rtk {
+#ifndef RTK_NS
+#define RTK_NS rtk
+#endif
+#ifndef RTK_HWMATH
+#define RTK_HWMATH 0
+#endif
+
+namespace RTK_NS {
 
 struct F3 {
     float x, y, z;
@@ -32,7 +44,11 @@ __device__ __forceinline__ F3 cross(F3 a, F3 b) {
     return F3{__builtin_fmaf(a.y, b.z, b.y * -a.z), __builtin_fmaf(a.z, b.x, b.z * -a.x),
               __builtin_fmaf(a.x, b.y, b.x * -a.y)};
 }
+#if RTK_HWMATH
+__device__ __forceinline__ float rsqrt_s(float x) { return ::rsqrtf(x); }
+#else
 __device__ __forceinline__ float rsqrt_s(float x) { return (float)(1.0 / ::sqrt((double)x)); }
+#endif
 
 // opencl.bc _Z9normalizeDv3_f (rsqrt substituted)
 __device__ __forceinline__ F3 normalize(F3 p) {
@@ -54,11 +70,20 @@ __device__ __forceinline__ F3 normalize(F3 p) {
     return p * rsqrt_s(l2);
 }
 
+#if RTK_HWMATH
+// OpenCL clamp -> __ockl_median3_f32 -> v_med3_f32 (identical to the line below for non-NaN x)
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+#else
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+#endif
+#if RTK_HWMATH
+__device__ __forceinline__ float pow5(float x) { return ::powf(x, 5.0f); }
+#else
 __device__ __forceinline__ float pow5(float x) {
     double d = (double)x;
     return (float)((((d * d) * d) * d) * d);
 }
+#endif
 
 // volumeRender.cl:25
 __device__ __forceinline__ F3 reflect(F3 i, F3 n) { return i - (2.0f * n) * dot(n, i); }
@@ -164,4 +189,4 @@ __device__ __forceinline__ uint32_t rgb_to_int(float r, float g, float b) {
     return ((uint32_t)b << 16) | ((uint32_t)g << 8) | (uint32_t)r;
 }
 
-}  // namespace rtk
+}  // namespace RTK_NS

@@ -32,7 +32,6 @@
 #include <vector>
 
 #include "rt_abi.h"
-#include "rt_device_math.h"
 
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 24
@@ -102,187 +101,22 @@ struct Stack {
     }
 };
 
-// traverse_bvh (volumeRender.cl:658-1010), reference visit order.
-template <bool CLOSEST>
-__device__ int traverse(const DevScene& S, const Ray& ray, float& tHit, const Stack& st, bool& overflow) {
-    uint32_t cur = S.root;
-    int sc = 1;            // stack_count; entry sc-1 is `cur`, entries 0..sc-2 are in `st`
-    int tri_index = -1;
-    const float ox = ray.ori.x, oy = ray.ori.y, oz = ray.ori.z;
-    const float dx = ray.dir.x, dy = ray.dir.y, dz = ray.dir.z;
-    while (true) {
-        if (cur & kLeafBit) {
-            int off, cnt;
-            leaf_range(S, cur, off, cnt);
-            const float4* tp = S.tris + (size_t)off * 3;
-            for (int i = 0; i < cnt; ++i) {
-                const float4 q0 = tp[3 * i + 0];
-                const float4 q1 = tp[3 * i + 1];
-                const float4 q2 = tp[3 * i + 2];
-                const float t = ray_tri(ray, F3{q0.x, q0.y, q0.z}, F3{q1.x, q1.y, q1.z}, F3{q2.x, q2.y, q2.z});
-                if (t < tHit && t > kTmin) {
-                    tHit = t;
-                    const int tri1 = __float_as_int(q0.w);
-                    if (!CLOSEST) return tri1;
-                    tri_index = tri1;
-                }
-            }
-            if (--sc == 0) break;
-            cur = st.get(sc - 1);
-            continue;
-        }
-        if (cur == kRefError) return -1;
-        const float4* np = S.wnodes + (size_t)cur * 4;
-        const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
-        // ray_box (volumeRender.cl:612-624) on both children, IEEE division
-        float n0, f0, n1, f1;
-        {
-            const float ax = (q0.x - ox) / dx, ay = (q0.y - oy) / dy, az = (q0.z - oz) / dz;
-            const float bx = (q0.w - ox) / dx, by = (q1.x - oy) / dy, bz = (q1.y - oz) / dz;
-            n0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-            f0 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-        }
-        {
-            const float ax = (q1.z - ox) / dx, ay = (q1.w - oy) / dy, az = (q2.x - oz) / dz;
-            const float bx = (q2.y - ox) / dx, by = (q2.z - oy) / dy, bz = (q2.w - oz) / dz;
-            n1 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-            f1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-        }
-        const bool i0 = (n0 <= f0) && (f0 >= kTmin) && (n0 <= tHit);
-        const bool i1 = (n1 <= f1) && (f1 >= kTmin) && (n1 <= tHit);
-        const uint32_t r0 = __float_as_uint(q3.x), r1 = __float_as_uint(q3.y);
-        if (i0 && i1) {
-            uint32_t nearr = r0, farr = r1;
-            if (n0 > n1) { nearr = r1; farr = r0; }
-            if (sc >= kStackSize) {  // volumeRender.cl:914
-                overflow = true;
-                return -1;
-            }
-            st.put(sc - 1, farr);
-            cur = nearr;
-            ++sc;
-        } else if (i0) {
-            cur = r0;
-        } else if (i1) {
-            cur = r1;
-        } else {
-            if (--sc == 0) break;
-            cur = st.get(sc - 1);
-        }
-    }
-    return tri_index;
-}
-
-__global__ void __launch_bounds__(256) render_kernel(DevScene S, Frame F, Outputs O, int want_aux) {
-    __shared__ uint32_t s_stack[kWavesPerBlock][kLdsStack][64];
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-
-    // XCD-aware block remap (bijective): blocks b, b+8, ... share an XCD; give
-    // each XCD a contiguous run of tiles.
-    const uint32_t nb = F.num_blocks, b = blockIdx.x;
-    const uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
-    const uint32_t tb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-    const uint32_t tx = tb % F.tiles_x, ty = tb / F.tiles_x;
-    const uint32_t x = tx * 16 + (wave & 1) * 8 + (lane & 7);
-    const uint32_t lr = ty * 16 + (wave >> 1) * 8 + (lane >> 3);
-    if (x >= F.w || lr >= F.local_rows) return;
-    uint32_t y = lr;
-    if (F.nranks > 1) {
-        const uint32_t band = lr / (uint32_t)F.band_rows, rib = lr % (uint32_t)F.band_rows;
-        y = (band * (uint32_t)F.nranks + (uint32_t)F.rank) * (uint32_t)F.band_rows + rib;
-    }
-    if (y >= F.h) return;
-    const uint64_t pix = (uint64_t)lr * F.w + x;
-
-    Stack st;
-    st.lds = &s_stack[wave][0][lane];
-    st.glb = O.gstack + pix;
-    st.gstride = O.local_pixels;
-    bool overflow = false;
-
-    const int depth = F.depth;
-    if (want_aux) {
-        for (int k = 0; k < depth; ++k) {
-            O.hits[(pix * depth + k) * 2 + 0] = -2;
-            O.hits[(pix * depth + k) * 2 + 1] = -2;
-            O.t[pix * depth + k] = -1.0f;
-        }
-    }
-
-    // volumeRender.cl:1169-1190
-    const float xf = (float)(((double)x - 0.5) / (double)(float)F.w);
-    const float yf = (float)(((double)y - 0.5) / (double)(float)F.h);
-    const F3 a = F3{F.a.x, F.a.y, F.a.z}, bb = F3{F.b.x, F.b.y, F.b.z}, c = F3{F.c.x, F.c.y, F.c.z};
-    const F3 campos = F3{F.campos.x, F.campos.y, F.campos.z};
-    const F3 light_pos = F3{F.light_pos.x, F.light_pos.y, F.light_pos.z};
-    const F3 t1 = c + a * xf;
-    const F3 t2 = bb * yf;
-    const F3 image_pos = t1 + t2;
-    Ray ray = ray_init(image_pos, image_pos - campos);
-    float tHit = 4294967296.0f;  // HitRecordInit: t = UINT_MAX
-    bool cont = ray_box_scene(F3{F.smin.x, F.smin.y, F.smin.z}, F3{F.smax.x, F.smax.y, F.smax.z}, ray.ori,
-                              ray.inv_dir);
-    F3 color = F3{0, 0, 0};
-    float shadow_sum = 0.0f;
-    int ray_depth = 0;
-    const bool do_shadow = !(F.flags & RT_FLAG_NO_SHADOW);
-    while (cont && ray_depth < depth) {
-        const int hit = traverse<true>(S, ray, tHit, st, overflow);
-        if (want_aux) {
-            O.hits[(pix * depth + ray_depth) * 2] = hit;
-            O.t[pix * depth + ray_depth] = tHit;
-        }
-        if (hit >= 0) {
-            const int kk = ray_depth;
-            ray_depth++;
-            const float4* sp = S.shade + (size_t)(hit / 3) * 7;
-            const float4 p0 = sp[0], p1 = sp[1], p2 = sp[2], m0 = sp[3], m1 = sp[4], m2 = sp[5], alb = sp[6];
-            const F3 vNew = ray.ori + ray.dir * (tHit - 0.001f);
-            const F3 normal = normalize(normal_at(vNew, xyz(p0), xyz(p1), xyz(p2), xyz(m0), xyz(m1), xyz(m2)));
-            const F3 l1 = normalize(light_pos - vNew);
-            const F3 v = normalize(ray.ori - vNew);
-            const F3 n = normalize(normal);
-            const F3 albedo = xyz(alb);
-            const float f0 = 40.0f * (1.0f / 255.0f);
-            F3 rez = cook_torrance_ggx(n, l1, v, albedo, f0, 0.5f) * 3.0f;
-            rez = rez + F3{0.3f, 0.3f, 0.3f} * albedo;
-            const F3 hitpoint = vNew;
-            const F3 L = normalize(light_pos - hitpoint);
-            float shadow_coef = 1.0f;
-            if (do_shadow) {
-                const Ray sray = ray_init(hitpoint + L * 0.001f, L);
-                float ts = 4294967296.0f;
-                const int sh = traverse<false>(S, sray, ts, st, overflow);
-                if (want_aux) O.hits[(pix * depth + kk) * 2 + 1] = sh;
-                if (sh >= 0 && ts > 0.025f) shadow_coef = 0.25f;
-            }
-            color = color + rez;
-            shadow_sum += shadow_coef;
-            const F3 refl = reflect(ray.dir, normal);
-            ray = ray_init(hitpoint + refl * 0.001f, refl);
-            tHit = 4294967296.0f;
-        } else {
-            cont = false;
-        }
-    }
-    if (ray_depth >= 1) {
-        color = color / (float)ray_depth;
-        shadow_sum /= (float)ray_depth;
-        color = color * shadow_sum;
-    } else {
-        color = F3{0, 0, 0};
-    }
-    if (want_aux) {
-        O.rgb[pix * 3 + 0] = color.x;
-        O.rgb[pix * 3 + 1] = color.y;
-        O.rgb[pix * 3 + 2] = color.z;
-    }
-    O.out[pix] = rgb_to_int(color.x * 255.0f, color.y * 255.0f, color.z * 255.0f);
-    if (overflow) atomicAdd(O.overflow, 1ull);
-}
-
 }  // namespace rtk
+
+// Two instantiations of the math + kernel: S_strict (default, CPU-reproducible)
+// and S_hw (RT_FLAG_HW_MATH: the device-library rsqrt/pow the reference links).
+#define RTK_NS rtk_strict
+#define RTK_HWMATH 0
+#include "rt_device_math.h"
+#include "rt_kernel_body.inc"
+#undef RTK_NS
+#undef RTK_HWMATH
+#define RTK_NS rtk_hw
+#define RTK_HWMATH 1
+#include "rt_device_math.h"
+#include "rt_kernel_body.inc"
+#undef RTK_NS
+#undef RTK_HWMATH
 
 // ============================================================================
 // Host side: context, upload/repack, launch.
@@ -583,7 +417,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.local_pixels = (uint64_t)npix;
 
     HIPC(c, hipEventRecord(c->ev0, s));
-    hipLaunchKernelGGL(rtk::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
+    if (flags & RT_FLAG_HW_MATH)
+        hipLaunchKernelGGL(rtk_hw::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
+    else
+        hipLaunchKernelGGL(rtk_strict::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
     HIPC(c, hipGetLastError());
     HIPC(c, hipEventRecord(c->ev1, s));
     c->timing_valid = true;

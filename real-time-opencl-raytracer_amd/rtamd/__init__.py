@@ -28,6 +28,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "librtamd.so")
 
 RT_FLAG_NO_SHADOW = 1
+RT_FLAG_HW_MATH = 2
 RT_MAX_DEPTH = 8
 ERRORS = {0: "RT_OK", -1: "RT_ERR_INVALID_ARG", -2: "RT_ERR_DEVICE", -3: "RT_ERR_NO_SCENE",
           -4: "RT_ERR_OUT_OF_MEMORY", -5: "RT_ERR_BAD_SCENE"}
@@ -91,6 +92,13 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RtError(-2, f"{LIB_PATH} not built (run __graft_entry__.build() or make -C {PKG_ROOT})")
+        # torch bundles its own libamdhip64.so.7 / libhsa-runtime64.so.1 (same SONAMEs as
+        # /opt/rocm's).  Let torch load them first so the process has ONE HIP runtime that
+        # both torch tensors (device memory, streams, RCCL) and librtamd.so use.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp, i32, u32, f32 = C.c_void_p, C.c_int32, C.c_uint32, C.c_float
         sig = {
@@ -112,7 +120,7 @@ def lib() -> C.CDLL:
             "rt_mesh_load_obj": (C.c_int, [vp, C.c_char_p]),
             "rt_mesh_gen_cornell": (C.c_int, [vp]),
             "rt_mesh_gen_torus_knot": (C.c_int, [vp, i32, i32]),
-            "rt_mesh_gen_heightfield": (C.c_int, [vp, i32, i32, f32, u32]),
+            "rt_mesh_gen_heightfield": (C.c_int, [vp, i32, i32, f32, u32, f32, f32, f32, f32]),
             "rt_mesh_gen_random": (C.c_int, [vp, i32, f32, f32, u32]),
             "rt_mesh_append_grid": (C.c_int, [vp, vp, i32, i32, f32, f32, f32]),
             "rt_bvh_build": (C.c_int, [vp, i32, i32, C.POINTER(vp)]),
@@ -218,8 +226,8 @@ class Mesh:
         m = cls(); _check(lib().rt_mesh_gen_torus_knot(m._h, nu, nv)); return m
 
     @classmethod
-    def heightfield(cls, nx=500, nz=1000, amplitude=10.0, seed=0x5EED) -> "Mesh":
-        m = cls(); _check(lib().rt_mesh_gen_heightfield(m._h, nx, nz, amplitude, seed)); return m
+    def heightfield(cls, nx=500, nz=1000, amplitude=10.0, seed=0x5EED, extent=(-100.0, 100.0, -100.0, 100.0)) -> "Mesh":
+        m = cls(); _check(lib().rt_mesh_gen_heightfield(m._h, nx, nz, amplitude, seed, *extent)); return m
 
     @classmethod
     def random(cls, ntris, extent=80.0, size=6.0, seed=1) -> "Mesh":

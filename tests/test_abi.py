@@ -1,0 +1,59 @@
+"""The C-ABI library loads and exports every function include/*.h declares (CPU;
+no compute calls)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import rtamd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(rt_\w+)\s*\(", txt, flags=re.M)
+    return sorted(set(names))
+
+
+def test_headers_declare_expected_symbols():
+    assert set(_declared("rt_abi.h")) == set(rtamd.ABI_SYMBOLS)
+    assert set(_declared("rt_host.h")) == set(rtamd.HOST_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = rtamd.lib()
+    for name in _declared("rt_abi.h") + _declared("rt_host.h"):
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", rtamd.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (rt_\w+)", out))
+    assert set(_declared("rt_abi.h")) <= exported
+    assert set(_declared("rt_host.h")) <= exported
+
+
+def test_abi_version_and_errors_without_gpu():
+    lib = rtamd.lib()
+    assert lib.rt_abi_version() == 1
+    assert lib.rt_set_params(None, None) == -1
+    assert lib.rt_render(None, 1, 1, 1, 0, None, None) == -1
+    assert rtamd.tiling_pixels(100, 50, 0, 1, 16) == 5000
+    # bands of 16 rows over 50 rows, 3 ranks: rank 0 owns bands 0 and 3 (16 + 2 rows)
+    assert rtamd.tiling_pixels(100, 50, 0, 3, 16) == 18 * 100
+    assert rtamd.tiling_pixels(100, 50, 1, 3, 16) == 16 * 100
+    assert sum(rtamd.tiling_pixels(100, 50, r, 3, 16) for r in range(3)) == 5000
+    assert rtamd.tiling_pixels(100, 50, 5, 3, 16) == -1
+
+
+def test_product_has_no_oracle_dependency():
+    """The product library must not link or reference the oracle."""
+    out = subprocess.run(["nm", "-D", rtamd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle_" not in out
+    deps = subprocess.run(["ldd", rtamd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in deps
+    uses = re.compile(r"(^\s*(from|import)\s+oracle)|(#\s*include\s*[<\"][^>\"]*oracle)|liboracle|oracle_render|"
+                      r"ref_ocl", re.M)
+    for root, _, files in os.walk(os.path.join(ROOT, "real-time-opencl-raytracer_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", ".inc", "Makefile")):
+                assert not uses.search(open(os.path.join(root, f)).read()), f
