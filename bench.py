@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extra-flags", type=int, default=0, help="OR-ed into rt_render flags (A/B: 2 = HW math, "
+                    "4 = IEEE-division slab test)")
     args = ap.parse_args()
 
     import torch
@@ -89,7 +91,7 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = CONFIGS[args.config]
-    w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"]
+    w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"] | args.extra_flags
 
     host_threads = max(1, min(16, (os.cpu_count() or 1)) // max(1, world))
     mesh, bvh, build_s = make_scene(cfg, host_threads)

@@ -68,10 +68,12 @@ enum {
 enum {
     RT_FLAG_NO_SHADOW = 1u,  /* config C2 "primary rays only": skip the any-hit shadow ray
                                 (volumeRender.cl:1437-1460); coefficient stays 1 */
-    RT_FLAG_HW_MATH = 2u     /* S_hw arithmetic: normalize's rsqrt and GGX's pow use the gfx950
+    RT_FLAG_HW_MATH = 2u,    /* S_hw arithmetic: normalize's rsqrt and GGX's pow use the gfx950
                                 device-library functions the reference kernel links
                                 (v_rsq_f32, __ocml_pow_f32) instead of the S_strict
                                 CPU-reproducible ones */
+    RT_FLAG_EXACT_DIV = 4u   /* force the IEEE-division slab test (volumeRender.cl:614-615) instead of
+                                the bit-identical 3-op fast quotient; for A/B only */
 };
 
 #define RT_MAX_DEPTH 8       /* reference: RAY_TRACE_DEPTH 3 (volumeRender.cl:12) */

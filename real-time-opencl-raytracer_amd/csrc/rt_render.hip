@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -54,6 +55,7 @@ struct DevScene {
     const float4* __restrict__ shade;    // [n_tris][7]
     const int2* __restrict__ leaf_table; // escape leaves {offset, count}
     uint32_t root;
+    int fast_div;                        // every box coordinate is 0 or in [2^-66, 2^60]
 };
 
 struct Frame {
@@ -131,6 +133,7 @@ struct rt_ctx {
     float4* d_shade = nullptr;
     int2* d_leaf = nullptr;
     uint32_t root = 0;
+    int fast_div = 0;
     bool have_scene = false;
     bool have_params = false;
     rt_params params{};
@@ -294,6 +297,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         }
         int32_t n_inner = next;
         std::vector<float4> wn((size_t)std::max(n_inner, 1) * 4, make_float4(0, 0, 0, 0));
+        bool fast_ok = true;  // slab-test fast exact division domain (rt_kernel_body.inc axis_ok)
         for (int32_t n = 0; n < nn; ++n) {
             if (inner_id[n] < 0) continue;
             const rt_bvh_node& L = nodes[nodes[n].offset_left];
@@ -307,6 +311,13 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             std::memcpy(&f0, &r0, 4);
             std::memcpy(&f1, &r1, 4);
             q[3] = make_float4(f0, f1, 0.0f, 0.0f);
+            for (int k = 0; k < 3; ++k) {
+                const float* qf = &q[k].x;
+                for (int j = 0; j < 4; ++j) {
+                    const float a = std::fabs(qf[j]);
+                    if (!(a == 0.0f || (a >= 0x1p-66f && a <= 0x1p60f))) fast_ok = false;
+                }
+            }
         }
         // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974)
         std::vector<float4> tr((size_t)std::max(nref, 1) * 3, make_float4(0, 0, 0, 0));
@@ -345,6 +356,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         HIPC(c, hipMemcpy(c->d_shade, sh.data(), sh.size() * sizeof(float4), hipMemcpyHostToDevice));
         HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
         c->root = ref_of[0];
+        c->fast_div = fast_ok ? 1 : 0;
         c->have_scene = true;
     }
     return RT_OK;
@@ -406,7 +418,8 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.tiles_y = (F.local_rows + 15) / 16;
     F.num_blocks = F.tiles_x * F.tiles_y;
 
-    rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root};
+    rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root,
+                    (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0};
     rtk::Outputs O;
     O.out = d_out;
     O.hits = aux ? d_aux->hits : nullptr;

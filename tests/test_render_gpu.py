@@ -131,3 +131,32 @@ def test_errors(renderer):
     with pytest.raises(rtamd.RtError):
         r.render(16, 16, depth=99)
     r.close()
+
+
+@pytest.mark.parametrize("name", ["hf40k", "knot16k", "cubes2_obj", "rand3k_bigleaf"])
+def test_fast_division_is_bit_identical(renderer, name):
+    """The 3-op slab quotient against the IEEE-division slab test."""
+    import rtamd
+    d = load_golden(name)
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    fast = renderer.render(w, h, depth=3, aux=True)
+    slow = renderer.render(w, h, depth=3, flags=rtamd.RT_FLAG_EXACT_DIV, aux=True)
+    _compare(fast, slow, name + " fast-vs-exact division")
+
+
+def test_tiny_coordinates_fall_back_to_division(renderer):
+    """A scene with a box coordinate below 2^-66 disables the fast quotient; results still match."""
+    import rtamd
+    v = np.array([[-40, -10, 1e-25, 1], [40, -10, 0, 1], [0, 50, 5, 1], [-30, 0, -30, 1], [30, 0, -30, 1],
+                  [0, 0, 30, 1]], np.float32)
+    m = rtamd.Mesh.from_arrays(v, np.arange(6, dtype=np.int32))
+    s = rtamd.Scene.from_mesh(m, m.build_bvh())
+    p = rtamd.params_to_array(m.camera_params(64, 64))
+    renderer.upload(s)
+    renderer.set_params(p)
+    gpu = renderer.render(64, 64, depth=3, aux=True)
+    from oracle import oracle
+    ref = oracle.render(s, p, 64, 64, depth=3)
+    _compare(gpu, ref, "tiny coordinates")
