@@ -128,18 +128,8 @@ def main():
 
     # band -> frame re-interleave (rank 0): gathered slot r holds rank r's bands in order
     def assemble():
-        if world == 1:
-            return
-        rows_per_rank = [rtamd.tiling_pixels(w, h, q, world, args.band_rows) // w for q in range(world)]
-        fv = frame.view(h, w)
-        for q in range(world):
-            src = gather[q].view(-1, w)
-            row = 0
-            for b in range(q, nbands, world):
-                n = min(args.band_rows, h - b * args.band_rows)
-                fv[b * args.band_rows:b * args.band_rows + n].copy_(src[row:row + n], non_blocking=True)
-                row += n
-            assert row == rows_per_rank[q]
+        if world > 1:
+            rtamd.assemble_bands(frame, gather, w, h, args.band_rows)
 
     def step():
         r.render_device(w, h, depth, flags, out.data_ptr(), tiling=tiling, stream=stream.cuda_stream)

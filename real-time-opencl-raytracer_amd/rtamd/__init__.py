@@ -388,3 +388,28 @@ class Renderer:
 def tiling_pixels(w: int, h: int, rank: int, nranks: int, band_rows: int) -> int:
     t = rt_tiling(rank, nranks, band_rows, 0)
     return int(lib().rt_tiling_pixels(w, h, C.byref(t)))
+
+
+def rank_bands(h: int, rank: int, nranks: int, band_rows: int):
+    """[(first global row, rows)] of the bands `rank` owns, in its buffer order
+    (band b belongs to rank b % nranks; same rule as rt_tiling in include/rt_abi.h)."""
+    nbands = (h + band_rows - 1) // band_rows
+    return [(b * band_rows, min(band_rows, h - b * band_rows)) for b in range(rank, nbands, nranks)]
+
+
+def assemble_bands(frame, chunks, w: int, h: int, band_rows: int):
+    """Re-interleave gathered per-rank band buffers into the frame (rank 0 after the
+    gather).  `frame` is (h*w,) and chunks[r] holds rank r's bands in order; works on
+    numpy arrays and on torch tensors (device copies stay on the device)."""
+    nranks = len(chunks)
+    fv = frame.reshape(h, w) if hasattr(frame, "reshape") else frame.view(h, w)
+    for r, ch in enumerate(chunks):
+        src = ch.reshape(-1, w) if not hasattr(ch, "view") or isinstance(ch, np.ndarray) else ch.view(-1, w)
+        row = 0
+        for y0, n in rank_bands(h, r, nranks, band_rows):
+            if isinstance(fv, np.ndarray):
+                fv[y0:y0 + n] = src[row:row + n]
+            else:
+                fv[y0:y0 + n].copy_(src[row:row + n], non_blocking=True)
+            row += n
+    return frame
