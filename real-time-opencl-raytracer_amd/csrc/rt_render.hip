@@ -37,6 +37,12 @@
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 24
 #endif
+#ifndef RTK_WHILE_WHILE
+#define RTK_WHILE_WHILE 1
+#endif
+#ifndef RTK_TRI_PREFETCH
+#define RTK_TRI_PREFETCH 1
+#endif
 
 namespace rtk {
 
