@@ -41,7 +41,10 @@
 #define RTK_WHILE_WHILE 1
 #endif
 #ifndef RTK_TRI_PREFETCH
-#define RTK_TRI_PREFETCH 1
+#define RTK_TRI_PREFETCH 0
+#endif
+#ifndef RTK_REFILL
+#define RTK_REFILL 16
 #endif
 
 namespace rtk {
@@ -73,6 +76,20 @@ struct Frame {
     uint32_t local_rows;
     uint32_t tiles_x, tiles_y, num_blocks;
 };
+
+// Pipelined path state (per local pixel) and work partitions.
+struct Pipe {
+    int2* hit_t;          // {closest hit id, t bits} of the current bounce
+    int* state;           // kAlive | ray_depth while the pixel still traces
+    float4* acc;          // colour.xyz, shadow_sum carried between bounces
+    float4* rays;         // [2] reflection ray {o, d} for the next bounce
+    uint32_t* heads;      // [2 * depth][16] partition fetch counters (zeroed per frame)
+    uint64_t n_slots;     // persistent lanes (global overflow-stack stride)
+    uint32_t n_items;     // 8x8-tile items covering the local frame
+    uint32_t part_items;  // items per partition (multiple of 64)
+    int bounce;
+};
+constexpr int kAlive = 0x40000000;
 
 struct Outputs {
     uint32_t* out;
@@ -149,6 +166,14 @@ struct rt_ctx {
     float* d_rgb = nullptr; size_t rgb_cap = 0;
     uint32_t* d_gstack = nullptr; size_t gstack_cap = 0;   // in pixels
     unsigned long long* d_overflow = nullptr;
+    // pipelined path buffers (per local pixel) + persistent grid sizes
+    int2* d_hit_t = nullptr; size_t hit_t_cap = 0;
+    int* d_state = nullptr; size_t state_cap = 0;
+    float4* d_acc = nullptr; size_t acc_cap = 0;
+    float4* d_rays = nullptr; size_t rays_cap = 0;
+    uint32_t* d_heads = nullptr; size_t heads_cap = 0;
+    uint32_t* d_pstack = nullptr; size_t pstack_cap = 0;
+    int grid_k1[2] = {0, 0}, grid_k2[2] = {0, 0};   // [strict, hw]
     float last_ms = 0.0f;
     bool timing_valid = false;
     std::string err;
@@ -224,6 +249,9 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_gstack) (void)hipFree(c->d_gstack);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
+    for (void* p : {(void*)c->d_hit_t, (void*)c->d_state, (void*)c->d_acc, (void*)c->d_rays, (void*)c->d_heads,
+                    (void*)c->d_pstack})
+        if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -399,8 +427,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         return set_err(c, "rt_render_device: aux needs hits, t and rgb together", RT_ERR_INVALID_ARG);
     HIPC(c, hipSetDevice(c->device));
     if (npix == 0) return RT_OK;
-    int rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack);
-    if (rc) return rc;
+    int rc = RT_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
 
     rtk::Frame F;
@@ -435,13 +462,71 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
 
-    HIPC(c, hipEventRecord(c->ev0, s));
-    if (flags & RT_FLAG_HW_MATH)
-        hipLaunchKernelGGL(rtk_hw::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
-    else
-        hipLaunchKernelGGL(rtk_strict::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
-    HIPC(c, hipGetLastError());
-    HIPC(c, hipEventRecord(c->ev1, s));
+    const bool hw = (flags & RT_FLAG_HW_MATH) != 0;
+    if ((flags & RT_FLAG_FUSED) || depth == 0) {
+        if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
+        O.gstack = c->d_gstack;
+        HIPC(c, hipEventRecord(c->ev0, s));
+        if (hw)
+            hipLaunchKernelGGL(rtk_hw::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
+        else
+            hipLaunchKernelGGL(rtk_strict::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
+        HIPC(c, hipGetLastError());
+        HIPC(c, hipEventRecord(c->ev1, s));
+    } else {
+        // persistent grids: blocks per CU from the occupancy query, x CUs, multiple of 8 (partitions)
+        const int mi = hw ? 1 : 0;
+        if (!c->grid_k1[mi]) {
+            int cus = 0, b1 = 0, b2 = 0;
+            HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+            if (hw) {
+                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_hw::trace_closest_kernel, 256, 0));
+                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, rtk_hw::shade_shadow_kernel, 256, 0));
+            } else {
+                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_strict::trace_closest_kernel, 256, 0));
+                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, rtk_strict::shade_shadow_kernel, 256, 0));
+            }
+            c->grid_k1[mi] = std::max(8, (std::max(b1, 1) * cus) & ~7);
+            c->grid_k2[mi] = std::max(8, (std::max(b2, 1) * cus) & ~7);
+        }
+        const int g1 = c->grid_k1[mi], g2 = c->grid_k2[mi];
+        const size_t slots = (size_t)std::max(g1, g2) * 256;
+        if ((rc = ensure(c, c->d_pstack, c->pstack_cap, slots * rtk::kGlobalStack))) return rc;
+        if ((rc = ensure(c, c->d_hit_t, c->hit_t_cap, (size_t)npix))) return rc;
+        if ((rc = ensure(c, c->d_state, c->state_cap, (size_t)npix))) return rc;
+        if (depth > 1) {
+            if ((rc = ensure(c, c->d_acc, c->acc_cap, (size_t)npix))) return rc;
+            if ((rc = ensure(c, c->d_rays, c->rays_cap, (size_t)npix * 2))) return rc;
+        }
+        if ((rc = ensure(c, c->d_heads, c->heads_cap, (size_t)2 * RT_MAX_DEPTH * 16))) return rc;
+        O.gstack = c->d_pstack;
+        rtk::Pipe Pp;
+        Pp.hit_t = c->d_hit_t;
+        Pp.state = c->d_state;
+        Pp.acc = c->d_acc;
+        Pp.rays = c->d_rays;
+        Pp.heads = c->d_heads;
+        Pp.n_slots = slots;
+        const uint32_t tiles = ((w + 7) / 8) * ((F.local_rows + 7) / 8);
+        Pp.n_items = tiles * 64;
+        Pp.part_items = ((tiles + 7) / 8) * 64;
+        HIPC(c, hipEventRecord(c->ev0, s));
+        HIPC(c, hipMemsetAsync(c->d_heads, 0, (size_t)2 * depth * 16 * sizeof(uint32_t), s));
+        for (int b = 0; b < depth; ++b) {
+            Pp.bounce = b;
+            if (hw) {
+                hipLaunchKernelGGL(rtk_hw::trace_closest_kernel, dim3(g1), dim3(256), 0, s, S, F, O, Pp, aux ? 1 : 0);
+                hipLaunchKernelGGL(rtk_hw::shade_shadow_kernel, dim3(g2), dim3(256), 0, s, S, F, O, Pp, aux ? 1 : 0);
+            } else {
+                hipLaunchKernelGGL(rtk_strict::trace_closest_kernel, dim3(g1), dim3(256), 0, s, S, F, O, Pp,
+                                   aux ? 1 : 0);
+                hipLaunchKernelGGL(rtk_strict::shade_shadow_kernel, dim3(g2), dim3(256), 0, s, S, F, O, Pp,
+                                   aux ? 1 : 0);
+            }
+            HIPC(c, hipGetLastError());
+        }
+        HIPC(c, hipEventRecord(c->ev1, s));
+    }
     c->timing_valid = true;
     return RT_OK;
 }

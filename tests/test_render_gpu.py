@@ -160,3 +160,17 @@ def test_tiny_coordinates_fall_back_to_division(renderer):
     from oracle import oracle
     ref = oracle.render(s, p, 64, 64, depth=3)
     _compare(gpu, ref, "tiny coordinates")
+
+
+@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("depth", [1, 3])
+def test_fused_and_pipelined_paths_agree(renderer, name, depth):
+    """RT_FLAG_FUSED (one kernel) and the default persistent pipeline give the same bits."""
+    import rtamd
+    d = load_golden(name)
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    pipe = renderer.render(w, h, depth=depth, aux=True)
+    fused = renderer.render(w, h, depth=depth, flags=rtamd.RT_FLAG_FUSED, aux=True)
+    _compare(pipe, fused, f"{name} depth={depth} pipelined-vs-fused")
