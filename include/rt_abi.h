@@ -72,8 +72,9 @@ enum {
                                 device-library functions the reference kernel links
                                 (v_rsq_f32, __ocml_pow_f32) instead of the S_strict
                                 CPU-reproducible ones */
-    RT_FLAG_FUSED = 8u,      /* single fused kernel (one lane = one pixel for the whole pipeline) instead
-                                of the persistent per-bounce trace / shade+shadow pipeline; A/B */
+    RT_FLAG_WAVEFRONT = 8u,  /* per-bounce persistent pipeline (closest-hit trace kernel, then shade +
+                                shadow-trace kernel, ballot refill of idle lanes) instead of the default
+                                fused one-lane-per-pixel kernel; bit-identical, currently slower */
     RT_FLAG_EXACT_DIV = 4u   /* force the IEEE-division slab test (volumeRender.cl:614-615) instead of
                                 the bit-identical 3-op fast quotient; for A/B only */
 };

@@ -46,6 +46,9 @@
 #ifndef RTK_REFILL
 #define RTK_REFILL 16
 #endif
+#ifndef RTK_XCD_CHUNK
+#define RTK_XCD_CHUNK 4
+#endif
 
 namespace rtk {
 
@@ -463,7 +466,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.local_pixels = (uint64_t)npix;
 
     const bool hw = (flags & RT_FLAG_HW_MATH) != 0;
-    if ((flags & RT_FLAG_FUSED) || depth == 0) {
+    if (!(flags & RT_FLAG_WAVEFRONT) || depth == 0) {
         if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
         O.gstack = c->d_gstack;
         HIPC(c, hipEventRecord(c->ev0, s));

@@ -165,12 +165,12 @@ def test_tiny_coordinates_fall_back_to_division(renderer):
 @pytest.mark.parametrize("name", golden_names())
 @pytest.mark.parametrize("depth", [1, 3])
 def test_fused_and_pipelined_paths_agree(renderer, name, depth):
-    """RT_FLAG_FUSED (one kernel) and the default persistent pipeline give the same bits."""
+    """The default fused kernel and RT_FLAG_WAVEFRONT (persistent per-bounce pipeline) give the same bits."""
     import rtamd
     d = load_golden(name)
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     w, h = int(d["w"]), int(d["h"])
-    pipe = renderer.render(w, h, depth=depth, aux=True)
-    fused = renderer.render(w, h, depth=depth, flags=rtamd.RT_FLAG_FUSED, aux=True)
+    fused = renderer.render(w, h, depth=depth, aux=True)
+    pipe = renderer.render(w, h, depth=depth, flags=rtamd.RT_FLAG_WAVEFRONT, aux=True)
     _compare(pipe, fused, f"{name} depth={depth} pipelined-vs-fused")
