@@ -35,7 +35,7 @@
 #include "rt_abi.h"
 
 #ifndef RTK_LDS_STACK
-#define RTK_LDS_STACK 24
+#define RTK_LDS_STACK 20
 #endif
 #ifndef RTK_WHILE_WHILE
 #define RTK_WHILE_WHILE 1
@@ -45,6 +45,12 @@
 #endif
 #ifndef RTK_REFILL
 #define RTK_REFILL 16
+#endif
+#ifndef RTK_FUSED_WAVES
+#define RTK_FUSED_WAVES 4   // waves per block of the fused kernel: 1, 2 or 4
+#endif
+#ifndef RTK_MIN_WAVES
+#define RTK_MIN_WAVES 6     // __launch_bounds__ minimum waves per SIMD (fused kernel)
 #endif
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
@@ -101,6 +107,8 @@ struct Outputs {
     float* rgb;
     uint32_t* gstack;            // [kGlobalStack][local_pixels]
     unsigned long long* overflow;
+    uint32_t* defer;             // pixels handed back by the fast kernel (render_list_kernel)
+    uint32_t* defer_count;
     uint64_t local_pixels;
 };
 
@@ -176,6 +184,7 @@ struct rt_ctx {
     float4* d_rays = nullptr; size_t rays_cap = 0;
     uint32_t* d_heads = nullptr; size_t heads_cap = 0;
     uint32_t* d_pstack = nullptr; size_t pstack_cap = 0;
+    uint32_t* d_defer = nullptr; size_t defer_cap = 0;       // [4 + P]: count, then deferred pixels
     int grid_k1[2] = {0, 0}, grid_k2[2] = {0, 0};   // [strict, hw]
     float last_ms = 0.0f;
     bool timing_valid = false;
@@ -253,7 +262,7 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_gstack) (void)hipFree(c->d_gstack);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
     for (void* p : {(void*)c->d_hit_t, (void*)c->d_state, (void*)c->d_acc, (void*)c->d_rays, (void*)c->d_heads,
-                    (void*)c->d_pstack})
+                    (void*)c->d_pstack, (void*)c->d_defer})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -450,8 +459,11 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.nranks = T->nranks > 1 ? T->nranks : 1;
     F.band_rows = T->nranks > 1 ? T->band_rows : 16;
     F.local_rows = (uint32_t)(npix / w);
-    F.tiles_x = (w + 15) / 16;
-    F.tiles_y = (F.local_rows + 15) / 16;
+    {
+        const uint32_t bw = RTK_FUSED_WAVES >= 2 ? 16 : 8, bh = RTK_FUSED_WAVES == 4 ? 16 : 8;
+        F.tiles_x = (w + bw - 1) / bw;
+        F.tiles_y = (F.local_rows + bh - 1) / bh;
+    }
     F.num_blocks = F.tiles_x * F.tiles_y;
 
     rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root,
@@ -469,11 +481,27 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     if (!(flags & RT_FLAG_WAVEFRONT) || depth == 0) {
         if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
         O.gstack = c->d_gstack;
+        if ((rc = ensure(c, c->d_defer, c->defer_cap, (size_t)npix + 4))) return rc;
+        O.defer = c->d_defer + 4;
+        O.defer_count = c->d_defer;
+        const bool fast_kernel = S.fast_div != 0;
+        const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
+        const int ax = aux ? 1 : 0;
         HIPC(c, hipEventRecord(c->ev0, s));
-        if (hw)
-            hipLaunchKernelGGL(rtk_hw::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
-        else
-            hipLaunchKernelGGL(rtk_strict::render_kernel, dim3(F.num_blocks), dim3(256), 0, s, S, F, O, aux ? 1 : 0);
+        if (fast_kernel) {
+            HIPC(c, hipMemsetAsync(c->d_defer, 0, 16, s));
+            if (hw) {
+                hipLaunchKernelGGL(rtk_hw::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
+                hipLaunchKernelGGL(rtk_hw::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
+            } else {
+                hipLaunchKernelGGL(rtk_strict::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
+                hipLaunchKernelGGL(rtk_strict::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
+            }
+        } else if (hw) {
+            hipLaunchKernelGGL(rtk_hw::render_kernel<false>, grid, block, 0, s, S, F, O, ax);
+        } else {
+            hipLaunchKernelGGL(rtk_strict::render_kernel<false>, grid, block, 0, s, S, F, O, ax);
+        }
         HIPC(c, hipGetLastError());
         HIPC(c, hipEventRecord(c->ev1, s));
     } else {

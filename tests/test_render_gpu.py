@@ -162,6 +162,31 @@ def test_tiny_coordinates_fall_back_to_division(renderer):
     _compare(gpu, ref, "tiny coordinates")
 
 
+def test_zero_direction_component_pixels_are_handed_back(renderer):
+    """An axis-aligned camera gives rays with a direction component exactly 0 (outside
+    the fast quotient's domain): the fast kernel hands those pixels to the general
+    kernel (render_list_kernel); the frame must still match the oracle."""
+    import rtamd
+    d = load_golden("knot16k")
+    s = _scene(d)
+    renderer.upload(s)
+    w = h = 65  # pixel 33: xf = 32.5 / 65 = 0.5 exactly -> image_pos.x == campos.x
+    p = np.zeros((8, 4), np.float32)
+    p[:, 3] = 1
+    p[0, :3] = [100, 0, 0]          # a
+    p[1, :3] = [0, 100, 0]          # b
+    p[2, :3] = [-50, -50, 120]      # c
+    p[3, :3] = [0, 0, 220]          # campos
+    p[4, :3] = [-23, 200, 3]
+    p[5, :3] = [1, 1, 1]
+    p[6, :3] = d["scene_min"]
+    p[7, :3] = d["scene_max"]
+    p = p.reshape(-1)
+    renderer.set_params(p)
+    gpu = renderer.render(w, h, depth=3, aux=True)
+    _compare(gpu, _oracle(d, 3, w=w, h=h, params=p), "axis-aligned camera")
+
+
 @pytest.mark.parametrize("name", golden_names())
 @pytest.mark.parametrize("depth", [1, 3])
 def test_fused_and_pipelined_paths_agree(renderer, name, depth):
