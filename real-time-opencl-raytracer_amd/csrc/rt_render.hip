@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -52,6 +53,9 @@
 #ifndef RTK_MIN_WAVES
 #define RTK_MIN_WAVES 6     // __launch_bounds__ minimum waves per SIMD (fused kernel)
 #endif
+#ifndef RTK_TILE_ORDER
+#define RTK_TILE_ORDER 1   // fused-kernel tile order policy (tile_order_table), env RTAMD_TILE_ORDER
+#endif
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
 #endif
@@ -74,6 +78,7 @@ struct DevScene {
     const int2* __restrict__ leaf_table; // escape leaves {offset, count}
     uint32_t root;
     int fast_div;                        // every box coordinate is 0 or in [2^-66, 2^60]
+    int clean;                           // no reachable malformed inner node (kRefError)
 };
 
 struct Frame {
@@ -84,6 +89,7 @@ struct Frame {
     int32_t rank, nranks, band_rows;
     uint32_t local_rows;
     uint32_t tiles_x, tiles_y, num_blocks;
+    const uint32_t* tile_order;   // [num_blocks] block -> tile, or null (in-kernel chunk dealing)
 };
 
 // Pipelined path state (per local pixel) and work partitions.
@@ -168,6 +174,7 @@ struct rt_ctx {
     int2* d_leaf = nullptr;
     uint32_t root = 0;
     int fast_div = 0;
+    int clean = 0;
     bool have_scene = false;
     bool have_params = false;
     rt_params params{};
@@ -185,6 +192,8 @@ struct rt_ctx {
     uint32_t* d_heads = nullptr; size_t heads_cap = 0;
     uint32_t* d_pstack = nullptr; size_t pstack_cap = 0;
     uint32_t* d_defer = nullptr; size_t defer_cap = 0;       // [4 + P]: count, then deferred pixels
+    uint32_t* d_order = nullptr; size_t order_cap = 0;        // tile order table for the fused kernel
+    uint32_t order_tx = 0, order_ty = 0; int order_policy = -1;
     int grid_k1[2] = {0, 0}, grid_k2[2] = {0, 0};   // [strict, hw]
     float last_ms = 0.0f;
     bool timing_valid = false;
@@ -222,6 +231,49 @@ static void free_scene(rt_ctx* c) {
     if (c->d_leaf) (void)hipFree(c->d_leaf);
     c->d_wnodes = nullptr; c->d_tris = nullptr; c->d_shade = nullptr; c->d_leaf = nullptr;
     c->have_scene = false;
+}
+
+// Block -> tile order of the fused kernel.  Blocks b, b+8, b+16, ... run on one
+// XCD (round-robin dispatch; a speed assumption only, never correctness).
+//   policy 0: none (in-kernel chunk dealing, RTK_XCD_CHUNK)
+//   policy 1: column strips -- XCD k gets the k-th eighth of the tile columns and
+//             walks it row by row, so all XCDs sweep the frame bottom-up together
+//             (balanced) while each L2 sees one compact screen region.
+static int tile_order_policy() {
+    const char* e = std::getenv("RTAMD_TILE_ORDER");
+    return e ? std::atoi(e) : RTK_TILE_ORDER;
+}
+
+static std::vector<uint32_t> tile_order_table(uint32_t tx, uint32_t ty, int policy) {
+    const uint32_t nb = tx * ty;
+    std::vector<uint32_t> order(nb);
+    if (policy != 1) {
+        for (uint32_t b = 0; b < nb; ++b) order[b] = b;
+        return order;
+    }
+    // per-XCD tile lists: XCD k owns columns [k*tx/8, (k+1)*tx/8), row-major within its strip
+    std::vector<std::vector<uint32_t>> want(8);
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t c0 = k * tx / 8, c1 = (k + 1) * tx / 8;
+        for (uint32_t y = 0; y < ty; ++y)
+            for (uint32_t x = c0; x < c1; ++x) want[k].push_back(y * tx + x);
+    }
+    // blocks of XCD k: b = k, k+8, ...; quota_k = number of such b below nb
+    std::vector<uint32_t> quota(8), cursor(8, 0);
+    for (uint32_t k = 0; k < 8; ++k) quota[k] = nb > k ? (nb - k + 7) / 8 : 0;
+    // surplus tiles of over-full strips go to XCDs with room, keeping row order (by tile index)
+    std::vector<uint32_t> spill;
+    for (uint32_t k = 0; k < 8; ++k)
+        while (want[k].size() > quota[k]) { spill.push_back(want[k].back()); want[k].pop_back(); }
+    std::sort(spill.begin(), spill.end());
+    size_t si = 0;
+    for (uint32_t k = 0; k < 8; ++k)
+        while (want[k].size() < quota[k] && si < spill.size()) want[k].push_back(spill[si++]);
+    for (uint32_t k = 0; k < 8; ++k) std::sort(want[k].begin(), want[k].end(), [tx](uint32_t a, uint32_t b) {
+        return a / tx != b / tx ? a / tx < b / tx : a < b;
+    });
+    for (uint32_t b = 0; b < nb; ++b) order[b] = want[b & 7][cursor[b & 7]++];
+    return order;
 }
 
 extern "C" {
@@ -262,7 +314,7 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_gstack) (void)hipFree(c->d_gstack);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
     for (void* p : {(void*)c->d_hit_t, (void*)c->d_state, (void*)c->d_acc, (void*)c->d_rays, (void*)c->d_heads,
-                    (void*)c->d_pstack, (void*)c->d_defer})
+                    (void*)c->d_pstack, (void*)c->d_defer, (void*)c->d_order})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -323,6 +375,10 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             state[n] = 2;
             stk.pop_back();
         }
+        bool clean = true;
+        for (int32_t n = 0; n < nn; ++n)
+            if (state[n] != 0 && nodes[n].offset_left >= 0 && inner_id[n] < 0) clean = false;
+        c->clean = clean ? 1 : 0;
         for (int32_t n = 0; n < nn; ++n) {
             const rt_bvh_node& nd = nodes[n];
             if (nd.offset_left >= 0) {
@@ -465,9 +521,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         F.tiles_y = (F.local_rows + bh - 1) / bh;
     }
     F.num_blocks = F.tiles_x * F.tiles_y;
+    F.tile_order = nullptr;
 
     rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root,
-                    (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0};
+                    (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0, c->clean};
     rtk::Outputs O;
     O.out = d_out;
     O.hits = aux ? d_aux->hits : nullptr;
@@ -484,7 +541,20 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         if ((rc = ensure(c, c->d_defer, c->defer_cap, (size_t)npix + 4))) return rc;
         O.defer = c->d_defer + 4;
         O.defer_count = c->d_defer;
-        const bool fast_kernel = S.fast_div != 0;
+        F.tile_order = nullptr;
+        const int pol = tile_order_policy();
+        if (pol != 0) {
+            if (c->order_policy != pol || c->order_tx != F.tiles_x || c->order_ty != F.tiles_y) {
+                const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y, pol);
+                if ((rc = ensure(c, c->d_order, c->order_cap, tab.size()))) return rc;
+                HIPC(c, hipMemcpy(c->d_order, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+                c->order_policy = pol;
+                c->order_tx = F.tiles_x;
+                c->order_ty = F.tiles_y;
+            }
+            F.tile_order = c->d_order;
+        }
+        const bool fast_kernel = S.fast_div != 0 && S.clean != 0;
         const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
         const int ax = aux ? 1 : 0;
         HIPC(c, hipEventRecord(c->ev0, s));
