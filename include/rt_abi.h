@@ -75,8 +75,11 @@ enum {
     RT_FLAG_WAVEFRONT = 8u,  /* per-bounce persistent pipeline (closest-hit trace kernel, then shade +
                                 shadow-trace kernel, ballot refill of idle lanes) instead of the default
                                 fused one-lane-per-pixel kernel; bit-identical, currently slower */
-    RT_FLAG_EXACT_DIV = 4u   /* force the IEEE-division slab test (volumeRender.cl:614-615) instead of
+    RT_FLAG_EXACT_DIV = 4u,  /* force the IEEE-division slab test (volumeRender.cl:614-615) instead of
                                 the bit-identical 3-op fast quotient; for A/B only */
+    RT_FLAG_STATIC_ORDER = 16u /* fused kernel: keep the static XCD-dealt block order instead of the
+                                adaptive longest-first order built from the previous frame's per-tile
+                                times; pixels are identical either way */
 };
 
 #define RT_MAX_DEPTH 8       /* reference: RAY_TRACE_DEPTH 3 (volumeRender.cl:12) */

@@ -51,10 +51,16 @@
 #define RTK_FUSED_WAVES 4   // waves per block of the fused kernel: 1, 2 or 4
 #endif
 #ifndef RTK_MIN_WAVES
-#define RTK_MIN_WAVES 6     // __launch_bounds__ minimum waves per SIMD (fused kernel)
+#define RTK_MIN_WAVES 7     // __launch_bounds__ minimum waves per SIMD (fused kernel)
 #endif
 #ifndef RTK_TILE_ORDER
 #define RTK_TILE_ORDER 1   // fused-kernel tile order policy (tile_order_table), env RTAMD_TILE_ORDER
+#endif
+#ifndef RTK_SCALAR_NODES
+#define RTK_SCALAR_NODES 0  // wave-uniform node / leaf fetches through the scalar cache (A/B: slower)
+#endif
+#ifndef RTK_WAVE_TIMES
+#define RTK_WAVE_TIMES 0    // diagnostic build: per-pixel start/end timestamps (env RTAMD_WAVE_TIMES=file)
 #endif
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
@@ -90,6 +96,7 @@ struct Frame {
     uint32_t local_rows;
     uint32_t tiles_x, tiles_y, num_blocks;
     const uint32_t* tile_order;   // [num_blocks] block -> tile, or null (in-kernel chunk dealing)
+    uint32_t* tile_cost;          // [num_blocks] per-tile wall time of this frame (adaptive order), or null
 };
 
 // Pipelined path state (per local pixel) and work partitions.
@@ -116,6 +123,7 @@ struct Outputs {
     uint32_t* defer;             // pixels handed back by the fast kernel (render_list_kernel)
     uint32_t* defer_count;
     uint64_t local_pixels;
+    uint32_t* wave_times;        // RTK_WAVE_TIMES diagnostic: per pixel {start, end, hw_id, xcc_id}
 };
 
 __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
@@ -191,9 +199,14 @@ struct rt_ctx {
     float4* d_rays = nullptr; size_t rays_cap = 0;
     uint32_t* d_heads = nullptr; size_t heads_cap = 0;
     uint32_t* d_pstack = nullptr; size_t pstack_cap = 0;
+    uint32_t* d_wt = nullptr; size_t wt_cap = 0;             // RTK_WAVE_TIMES
     uint32_t* d_defer = nullptr; size_t defer_cap = 0;       // [4 + P]: count, then deferred pixels
     uint32_t* d_order = nullptr; size_t order_cap = 0;        // tile order table for the fused kernel
     uint32_t order_tx = 0, order_ty = 0; int order_policy = -1;
+    uint32_t* d_cost = nullptr; size_t cost_cap = 0;          // adaptive order: last frame's per-tile times
+    uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;            //   and the longest-first order built from them
+    uint64_t cost_key = 0; bool cost_ready = false;
+    uint32_t scene_gen = 0;                                   // bumped by every upload
     int grid_k1[2] = {0, 0}, grid_k2[2] = {0, 0};   // [strict, hw]
     float last_ms = 0.0f;
     bool timing_valid = false;
@@ -314,7 +327,8 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_gstack) (void)hipFree(c->d_gstack);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
     for (void* p : {(void*)c->d_hit_t, (void*)c->d_state, (void*)c->d_acc, (void*)c->d_rays, (void*)c->d_heads,
-                    (void*)c->d_pstack, (void*)c->d_defer, (void*)c->d_order})
+                    (void*)c->d_pstack, (void*)c->d_defer, (void*)c->d_order, (void*)c->d_wt,
+                    (void*)c->d_cost, (void*)c->d_lpt})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -405,9 +419,10 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             const rt_bvh_node& L = nodes[nodes[n].offset_left];
             const rt_bvh_node& R = nodes[nodes[n].offset_right];
             float4* q = &wn[(size_t)inner_id[n] * 4];
-            q[0] = make_float4(L.min.x, L.min.y, L.min.z, L.max.x);
-            q[1] = make_float4(L.max.y, L.max.z, R.min.x, R.min.y);
-            q[2] = make_float4(R.min.z, R.max.x, R.max.y, R.max.z);
+            // axis-major: {L.min, R.min, L.max, R.max} per axis (rt_kernel_body.inc slab2)
+            q[0] = make_float4(L.min.x, R.min.x, L.max.x, R.max.x);
+            q[1] = make_float4(L.min.y, R.min.y, L.max.y, R.max.y);
+            q[2] = make_float4(L.min.z, R.min.z, L.max.z, R.max.z);
             uint32_t r0 = ref_of[nodes[n].offset_left], r1 = ref_of[nodes[n].offset_right];
             float f0, f1;
             std::memcpy(&f0, &r0, 4);
@@ -460,6 +475,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         c->root = ref_of[0];
         c->fast_div = fast_ok ? 1 : 0;
         c->have_scene = true;
+        ++c->scene_gen;
     }
     return RT_OK;
 }
@@ -522,6 +538,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     }
     F.num_blocks = F.tiles_x * F.tiles_y;
     F.tile_order = nullptr;
+    F.tile_cost = nullptr;
 
     rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root,
                     (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0, c->clean};
@@ -533,6 +550,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.gstack = c->d_gstack;
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
+    O.wave_times = nullptr;
 
     const bool hw = (flags & RT_FLAG_HW_MATH) != 0;
     if (!(flags & RT_FLAG_WAVEFRONT) || depth == 0) {
@@ -541,6 +559,13 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         if ((rc = ensure(c, c->d_defer, c->defer_cap, (size_t)npix + 4))) return rc;
         O.defer = c->d_defer + 4;
         O.defer_count = c->d_defer;
+#if RTK_WAVE_TIMES
+        if (std::getenv("RTAMD_WAVE_TIMES")) {
+            if ((rc = ensure(c, c->d_wt, c->wt_cap, (size_t)npix * 4))) return rc;
+            HIPC(c, hipMemsetAsync(c->d_wt, 0, (size_t)npix * 16, s));
+            O.wave_times = c->d_wt;
+        }
+#endif
         F.tile_order = nullptr;
         const int pol = tile_order_policy();
         if (pol != 0) {
@@ -554,10 +579,33 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             }
             F.tile_order = c->d_order;
         }
+        // Adaptive longest-first order (tile_order_kernel) from the previous frame of
+        // the same geometry; the first frame runs the static order and measures.
+        F.tile_cost = nullptr;
+        bool lpt = false;
+        if (!(flags & RT_FLAG_STATIC_ORDER)) {
+            if ((rc = ensure(c, c->d_cost, c->cost_cap, F.num_blocks))) return rc;
+            if ((rc = ensure(c, c->d_lpt, c->lpt_cap, F.num_blocks))) return rc;
+            const uint64_t key = ((uint64_t)F.tiles_x << 48) ^ ((uint64_t)F.tiles_y << 32) ^ F.local_rows ^
+                                 ((uint64_t)c->scene_gen << 20);
+            if (key != c->cost_key) {
+                HIPC(c, hipMemsetAsync(c->d_cost, 0, (size_t)F.num_blocks * 4, s));
+                c->cost_key = key;
+                c->cost_ready = false;
+            }
+            lpt = c->cost_ready;
+            F.tile_cost = c->d_cost;
+        }
         const bool fast_kernel = S.fast_div != 0 && S.clean != 0;
         const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
         const int ax = aux ? 1 : 0;
         HIPC(c, hipEventRecord(c->ev0, s));
+        if (lpt) {
+            hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt,
+                               F.num_blocks);
+            F.tile_order = c->d_lpt;
+        }
+        if (F.tile_cost) c->cost_ready = true;
         if (fast_kernel) {
             HIPC(c, hipMemsetAsync(c->d_defer, 0, 16, s));
             if (hw) {
@@ -574,6 +622,17 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         }
         HIPC(c, hipGetLastError());
         HIPC(c, hipEventRecord(c->ev1, s));
+#if RTK_WAVE_TIMES
+        if (O.wave_times) {
+            HIPC(c, hipStreamSynchronize(s));
+            std::vector<uint32_t> wt((size_t)npix * 4);
+            HIPC(c, hipMemcpy(wt.data(), O.wave_times, wt.size() * 4, hipMemcpyDeviceToHost));
+            if (FILE* f = std::fopen(std::getenv("RTAMD_WAVE_TIMES"), "wb")) {
+                std::fwrite(wt.data(), 4, wt.size(), f);
+                std::fclose(f);
+            }
+        }
+#endif
     } else {
         // persistent grids: blocks per CU from the occupancy query, x CUs, multiple of 8 (partitions)
         const int mi = hw ? 1 : 0;

@@ -30,6 +30,7 @@ LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(PKG_ROOT, "lib", "librtam
 RT_FLAG_NO_SHADOW = 1
 RT_FLAG_HW_MATH = 2
 RT_FLAG_EXACT_DIV = 4
+RT_FLAG_STATIC_ORDER = 16
 RT_FLAG_WAVEFRONT = 8
 RT_MAX_DEPTH = 8
 ERRORS = {0: "RT_OK", -1: "RT_ERR_INVALID_ARG", -2: "RT_ERR_DEVICE", -3: "RT_ERR_NO_SCENE",

@@ -199,3 +199,20 @@ def test_fused_and_pipelined_paths_agree(renderer, name, depth):
     fused = renderer.render(w, h, depth=depth, aux=True)
     pipe = renderer.render(w, h, depth=depth, flags=rtamd.RT_FLAG_WAVEFRONT, aux=True)
     _compare(pipe, fused, f"{name} depth={depth} pipelined-vs-fused")
+
+
+@pytest.mark.parametrize("name", ["hf40k", "knot16k"])
+def test_adaptive_block_order_is_bit_identical(renderer, name):
+    """Frames after the first run blocks longest-first from the previous frame's per-tile
+    times (tile_order_kernel); RT_FLAG_STATIC_ORDER keeps the static order.  Same pixels."""
+    import rtamd
+    d = load_golden(name)
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    static = renderer.render(w, h, depth=3, flags=rtamd.RT_FLAG_STATIC_ORDER, aux=True)
+    first = renderer.render(w, h, depth=3, aux=True)   # measures
+    second = renderer.render(w, h, depth=3, aux=True)  # longest-first order
+    _compare(first, static, name + " first adaptive frame")
+    _compare(second, static, name + " adaptive order")
+    _compare(second, _oracle(d, 3), name + " adaptive vs oracle")
