@@ -62,6 +62,9 @@
 #ifndef RTK_WAVE_TIMES
 #define RTK_WAVE_TIMES 0    // diagnostic build: per-pixel start/end timestamps (env RTAMD_WAVE_TIMES=file)
 #endif
+#ifndef RTK_PROBE_EXTRA_LOAD
+#define RTK_PROBE_EXTRA_LOAD 0
+#endif
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
 #endif
