@@ -33,7 +33,7 @@ CONFIGS = {
     # BASELINE.json configs[2] -- the metric's configuration
     "c3": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=HF_EXT, w=1920, h=1080, depth=1, flags=0,
                desc="C3: 1M-tri value-noise heightfield (500x1000 cells x2, seed 0x5EED), 1920x1080, "
-                    "primary + 1 shadow ray, binned-SAH BVH"),
+                    "primary + 1 shadow ray"),
     # configs[1]: ~70k-tri mesh, primary only
     "c2": dict(scene="knot", nu=256, nv=137, w=1920, h=1080, depth=1, flags=1,
                desc="C2: 70,144-tri torus knot, 1920x1080, primary rays only"),
@@ -46,7 +46,7 @@ CONFIGS = {
 }
 
 
-def make_scene(cfg, threads):
+def make_scene(cfg, threads, builder="sbvh"):
     import rtamd
     if cfg["scene"] == "heightfield":
         mesh = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"], cfg["ext"])
@@ -59,7 +59,7 @@ def make_scene(cfg, threads):
     else:
         raise ValueError(cfg["scene"])
     t0 = time.time()
-    bvh = mesh.build_bvh(8, threads)
+    bvh = mesh.build_sbvh(threads) if builder == "sbvh" else mesh.build_bvh(8, threads)
     return mesh, bvh, time.time() - t0
 
 
@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--bvh", default="sbvh", choices=["sbvh", "binned"],
+                    help="sbvh: the reference's SplitBVHBuilder (same bytes); binned: binned-SAH object splits")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra-flags", type=int, default=0, help="OR-ed into rt_render flags (A/B: 2 = HW math, "
@@ -94,7 +96,7 @@ def main():
     w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"] | args.extra_flags
 
     host_threads = max(1, min(16, (os.cpu_count() or 1)) // max(1, world))
-    mesh, bvh, build_s = make_scene(cfg, host_threads)
+    mesh, bvh, build_s = make_scene(cfg, host_threads, args.bvh)
     scene = rtamd.Scene.from_mesh(mesh, bvh)
     params = rtamd.params_to_array(mesh.camera_params(w, h))
     r = rtamd.Renderer(local)
@@ -240,7 +242,9 @@ def main():
                    "bvh_nodes": int(bvh.nodes.shape[0]), "width": w, "height": h, "depth": depth,
                    "shadow": not (flags & 1), "rays_per_frame": int(rays_total),
                    "primary_rays_per_frame": int(prim_total), "parallelism": f"screen bands x{world} (RCCL gather)",
-                   "band_rows": args.band_rows, "bvh_build_s": round(build_s, 3)},
+                   "band_rows": args.band_rows, "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)"
+                                                        if args.bvh == "sbvh" else "binned SAH"),
+                   "bvh_refs": int(bvh.tri_indices.size), "bvh_build_s": round(build_s, 3)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_ray": round(bpr, 1), "kernel_ms": round(kernel_ms_avg, 4),

@@ -5,10 +5,10 @@
  *   Mesh       (Mesh.h:69-101, Mesh.cpp:10-141)   indices/vertices/normals/materials
  *   BVH arrays (BVH_Cuda.h:87-137)                 BVH_Node_[] + tri_indices[] (= 3*tri)
  *   Params     (Camera.cpp:6-68, RayTracer.cpp:609-672)
- * The BVH builder here is this framework's own binned-SAH builder (object
- * splits, leaf size 1..8, SAH node/tri cost 1/1 as BVH2.cpp:11-20); it emits
- * the reference's node layout and ordering but is not the reference's
- * spatial-split builder.
+ * Two BVH builders: rt_bvh_build_sbvh is the reference's spatial-split
+ * builder (same bytes, parallel); rt_bvh_build is this framework's own
+ * binned-SAH builder (object splits only, leaf size 1..8, SAH node/tri cost
+ * 1/1 as BVH2.cpp:11-20) in the reference's node layout and ordering.
  */
 #ifndef RT_HOST_H
 #define RT_HOST_H
@@ -70,6 +70,12 @@ int rt_mesh_append_grid(rt_mesh* dst, const rt_mesh* src, int32_t gx, int32_t gz
 
 /* Binned-SAH BVH over the mesh; emits BVH_Node_ pre-order + tri_indices (x3). */
 int rt_bvh_build(const rt_mesh* m, int32_t max_leaf, int32_t num_threads, rt_bvh** out);
+/* The reference's spatial-split BVH: FW::BVH2(mesh) -> SplitBVHBuilder::run
+ * (SplitBVHBuilder.cpp:41-476, BVH2.cpp:11-31) -> BVH_Cuda::build_from_bvh2
+ * (BVH_Cuda.h:87-137).  Same BVH_Node_ and tri_indices bytes, built in
+ * parallel (num_threads <= 0: all cores); replaces the reference's
+ * single-threaded 317 s build of a 1M-triangle mesh. */
+int rt_bvh_build_sbvh(const rt_mesh* m, int32_t num_threads, rt_bvh** out);
 int rt_bvh_view_get(const rt_bvh* b, rt_bvh_view* out);
 void rt_bvh_destroy(rt_bvh* b);
 /* BVH cache file (nodes + refs + mesh hash), SURVEY.md 5 "checkpoint". */

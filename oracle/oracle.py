@@ -53,6 +53,10 @@ def lib():
         L.oracle_ray_tri.argtypes = [vp, vp, vp, vp, vp]
         L.oracle_rgb_to_int.restype = C.c_uint32
         L.oracle_rgb_to_int.argtypes = [C.c_float, C.c_float, C.c_float]
+        L.sbvh_oracle_build.restype = C.c_int
+        L.sbvh_oracle_build.argtypes = [vp, C.c_int32, vp, C.c_int32, C.POINTER(vp), C.POINTER(C.c_int32),
+                                        C.POINTER(C.POINTER(C.c_int32)), C.POINTER(C.c_int32)]
+        L.sbvh_oracle_free.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -96,6 +100,26 @@ def render(scene, params, w, h, depth=3, flags=0, pixels=None, nthreads=None, au
     if aux:
         res.update(hits=hits[:, :depth], t=tv[:, :depth], rgb=rgb)
     return res
+
+
+def sbvh(vertices, indices):
+    """The reference's SplitBVHBuilder + BVH_Cuda::build_from_bvh2 restated (sbvh_oracle.c).
+    vertices: float32 [nv, 4]; indices: int32 [3 * ntri].  Returns (nodes [nn, 12] float32 view of
+    BVH_Node_ records, tri_indices int32 (= 3 * triangle))."""
+    L = lib()
+    v = np.ascontiguousarray(vertices, np.float32).reshape(-1, 4)
+    ix = np.ascontiguousarray(indices, np.int32).reshape(-1)
+    nodes_p, refs_p = C.c_void_p(), C.POINTER(C.c_int32)()
+    nn, nr = C.c_int32(), C.c_int32()
+    rc = L.sbvh_oracle_build(_p(v), v.shape[0], _p(ix), ix.size // 3, C.byref(nodes_p), C.byref(nn),
+                             C.byref(refs_p), C.byref(nr))
+    if rc != 0:
+        raise RuntimeError("sbvh_oracle_build failed")
+    nodes = np.ctypeslib.as_array(C.cast(nodes_p, C.POINTER(C.c_float)), (max(nn.value, 1) * 12,)).copy()
+    refs = np.ctypeslib.as_array(refs_p, (max(nr.value, 1),)).copy()[:nr.value]
+    L.sbvh_oracle_free(nodes_p)
+    L.sbvh_oracle_free(C.cast(refs_p, C.c_void_p))
+    return nodes.reshape(-1, 12)[:nn.value], refs
 
 
 def bytes_per_ray(stats: dict, kind: str) -> float:

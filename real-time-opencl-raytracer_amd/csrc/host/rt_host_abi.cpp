@@ -105,6 +105,15 @@ int rt_bvh_build(const rt_mesh* mh, int32_t max_leaf, int32_t num_threads, rt_bv
     return RT_OK;
 }
 
+int rt_bvh_build_sbvh(const rt_mesh* mh, int32_t num_threads, rt_bvh** out) {
+    if (!mh || !out) return RT_ERR_INVALID_ARG;
+    rt_bvh* b = new (std::nothrow) rt_bvh();
+    if (!b) return RT_ERR_OUT_OF_MEMORY;
+    rtamd::build_sbvh(mh->m, num_threads, b->b);
+    *out = b;
+    return RT_OK;
+}
+
 int rt_bvh_view_get(const rt_bvh* bh, rt_bvh_view* o) {
     if (!bh || !o) return RT_ERR_INVALID_ARG;
     o->nodes = bh->b.nodes.data(); o->num_nodes = (int32_t)bh->b.nodes.size();

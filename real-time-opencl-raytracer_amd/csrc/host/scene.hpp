@@ -49,6 +49,8 @@ void gen_random(Mesh& m, int ntris, float extent, float size, uint32_t seed);
 void append_grid(Mesh& dst, const Mesh& src, int gx, int gz, float dx, float dz, float scale);
 
 void build_bvh(const Mesh& m, int max_leaf, int num_threads, Bvh& out);
+// The reference SplitBVHBuilder (SplitBVHBuilder.cpp:41-476) + BVH_Cuda::build_from_bvh2, same bytes.
+void build_sbvh(const Mesh& m, int num_threads, Bvh& out);
 
 rt_params camera_params(const Mesh& m, uint32_t w, uint32_t h, float radius, float extra_alpha,
                         float extra_beta, const float* light_pos, const float* light_color);

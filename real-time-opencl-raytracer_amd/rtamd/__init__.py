@@ -83,7 +83,7 @@ ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_gen_cornell", "rt_mesh_gen_torus_knot", "rt_mesh_gen_heightfield", "rt_mesh_gen_random",
-                "rt_mesh_append_grid", "rt_bvh_build", "rt_bvh_view_get", "rt_bvh_destroy", "rt_bvh_save",
+                "rt_mesh_append_grid", "rt_bvh_build", "rt_bvh_build_sbvh", "rt_bvh_view_get", "rt_bvh_destroy", "rt_bvh_save",
                 "rt_bvh_load", "rt_camera_params"]
 
 _lib = None
@@ -127,6 +127,7 @@ def lib() -> C.CDLL:
             "rt_mesh_gen_random": (C.c_int, [vp, i32, f32, f32, u32]),
             "rt_mesh_append_grid": (C.c_int, [vp, vp, i32, i32, f32, f32, f32]),
             "rt_bvh_build": (C.c_int, [vp, i32, i32, C.POINTER(vp)]),
+            "rt_bvh_build_sbvh": (C.c_int, [vp, i32, C.POINTER(vp)]),
             "rt_bvh_view_get": (C.c_int, [vp, C.POINTER(rt_bvh_view)]),
             "rt_bvh_destroy": (None, [vp]),
             "rt_bvh_save": (C.c_int, [vp, vp, C.c_char_p]),
@@ -288,6 +289,12 @@ class Mesh:
     def build_bvh(self, max_leaf: int = 8, threads: int = 0) -> "Bvh":
         h = C.c_void_p()
         _check(lib().rt_bvh_build(self._h, max_leaf, threads, C.byref(h)))
+        return Bvh(h)
+
+    def build_sbvh(self, threads: int = 0) -> "Bvh":
+        """The reference's SplitBVHBuilder BVH (SplitBVHBuilder.cpp:41-476 + BVH_Cuda.h:87-137), same bytes."""
+        h = C.c_void_p()
+        _check(lib().rt_bvh_build_sbvh(self._h, threads, C.byref(h)))
         return Bvh(h)
 
     def load_bvh(self, path: str) -> "Bvh":

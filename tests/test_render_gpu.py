@@ -216,3 +216,18 @@ def test_adaptive_block_order_is_bit_identical(renderer, name):
     _compare(first, static, name + " first adaptive frame")
     _compare(second, static, name + " adaptive order")
     _compare(second, _oracle(d, 3), name + " adaptive vs oracle")
+
+
+@pytest.mark.parametrize("make", ["random_splits", "knot"])
+def test_sbvh_scene_parity(renderer, make):
+    """Scenes on the reference's spatial-split BVH (duplicated references, rt_bvh_build_sbvh)."""
+    import rtamd
+    from oracle import oracle
+    m = rtamd.Mesh.random(6000, 100.0, 12.0, 3) if make == "random_splits" else rtamd.Mesh.torus_knot(96, 40)
+    s = rtamd.Scene.from_mesh(m, m.build_sbvh())
+    w, h = 96, 64
+    p = rtamd.params_to_array(m.camera_params(w, h))
+    renderer.upload(s)
+    renderer.set_params(p)
+    gpu = renderer.render(w, h, depth=3, aux=True)
+    _compare(gpu, oracle.render(s, p, w, h, depth=3), "sbvh " + make)
