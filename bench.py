@@ -42,11 +42,16 @@ CONFIGS = {
                desc="C4: C3 scene at 3840x2160, primary + 1 shadow ray"),
     # configs[4]: 10M tris (10 x C3 on a 5x2 grid), depth 3 (primary + 2 bounces, shadows)
     "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920, h=1080, depth=3, flags=0,
+               dae=False,  # a 1 GB Collada text file is not worth the round trip; built in memory
                desc="C5: 10M-tri merged scene (10 x C3 on a 5x2 grid), 1920x1080, 3 bounces with shadows"),
 }
 
 
-def make_scene(cfg, threads, builder="sbvh"):
+def make_scene(cfg, threads, builder="sbvh", via_dae=True):
+    """The config's synthetic mesh; with via_dae (configs C2-C4) it is written
+    as the reference-subset Collada file and read back through the ColladaLoader path
+    (rt_mesh_save_dae / rt_mesh_load_dae), as the reference application loads its scene."""
+    import tempfile
     import rtamd
     if cfg["scene"] == "heightfield":
         mesh = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"], cfg["ext"])
@@ -58,6 +63,11 @@ def make_scene(cfg, threads, builder="sbvh"):
         mesh.append_grid(tile, 5, 2, 160.0, 400.0, 1.0)
     else:
         raise ValueError(cfg["scene"])
+    if via_dae and cfg.get("dae", True):
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "scene.dae")
+            mesh.save_dae(path)
+            mesh = rtamd.Mesh.load_dae(path)
     t0 = time.time()
     bvh = mesh.build_sbvh(threads) if builder == "sbvh" else mesh.build_bvh(8, threads)
     return mesh, bvh, time.time() - t0
@@ -70,6 +80,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--direct", action="store_true", help="skip the Collada write/read of the scene")
     ap.add_argument("--bvh", default="sbvh", choices=["sbvh", "binned"],
                     help="sbvh: the reference's SplitBVHBuilder (same bytes); binned: binned-SAH object splits")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
@@ -96,7 +107,7 @@ def main():
     w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"] | args.extra_flags
 
     host_threads = max(1, min(16, (os.cpu_count() or 1)) // max(1, world))
-    mesh, bvh, build_s = make_scene(cfg, host_threads, args.bvh)
+    mesh, bvh, build_s = make_scene(cfg, host_threads, args.bvh, not args.direct)
     scene = rtamd.Scene.from_mesh(mesh, bvh)
     params = rtamd.params_to_array(mesh.camera_params(w, h))
     r = rtamd.Renderer(local)
@@ -244,7 +255,9 @@ def main():
                    "primary_rays_per_frame": int(prim_total), "parallelism": f"screen bands x{world} (RCCL gather)",
                    "band_rows": args.band_rows, "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)"
                                                         if args.bvh == "sbvh" else "binned SAH"),
-                   "bvh_refs": int(bvh.tri_indices.size), "bvh_build_s": round(build_s, 3)},
+                   "bvh_refs": int(bvh.tri_indices.size), "bvh_build_s": round(build_s, 3),
+                   "scene_source": "Collada (rt_mesh_load_dae)" if (cfg.get("dae", True) and not args.direct)
+                   else "in-memory generator"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_ray": round(bpr, 1), "kernel_ms": round(kernel_ms_avg, 4),

@@ -55,6 +55,15 @@ int rt_mesh_set(rt_mesh* m, const rt_float4* verts, int32_t nv, const int32_t* i
  * `v`, `vn`, `f a b c`, `f a//n b//n c//n`, `f a/t/n ...`; then Mesh::init(TriangleMesh&)
  * (Mesh.cpp:80-130): indices -1, normals normalized; default material. */
 int rt_mesh_load_obj(rt_mesh* m, const char* path);
+/* Collada subset, as the reference's ColladaLoader::load (ColladaLoader.cpp:13-593)
+ * followed by Mesh::init(ColladaLoader&) (Mesh.cpp:10-78): effects -> materials,
+ * first <polygons> of each geometry (9-int <p> per triangle), per-node matrix or
+ * rotate/translate transform; linear time (the reference's lookups are O(n^2)).
+ * Quirks and deviations are listed in csrc/host/collada.cpp. */
+int rt_mesh_load_dae(rt_mesh* m, const char* path);
+/* Writes the mesh as that Collada subset (the synthetic-scene generator of
+ * SURVEY.md 8d); rt_mesh_load_dae reads it back to the same arrays. */
+int rt_mesh_save_dae(const rt_mesh* m, const char* path);
 
 /* Synthetic scenes. All fit the reference's default
  * orbit camera (radius 200 around the origin). */

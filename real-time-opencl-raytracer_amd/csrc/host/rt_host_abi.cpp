@@ -68,6 +68,26 @@ int rt_mesh_load_obj(rt_mesh* mh, const char* path) {
     return RT_OK;
 }
 
+int rt_mesh_load_dae(rt_mesh* mh, const char* path) {
+    if (!mh || !path) return RT_ERR_INVALID_ARG;
+    std::string err;
+    if (rtamd::load_dae(path, mh->m, err) != 0) {
+        std::fprintf(stderr, "rt_mesh_load_dae: %s\n", err.c_str());
+        return RT_ERR_BAD_SCENE;
+    }
+    return RT_OK;
+}
+
+int rt_mesh_save_dae(const rt_mesh* mh, const char* path) {
+    if (!mh || !path) return RT_ERR_INVALID_ARG;
+    std::string err;
+    if (rtamd::save_dae(path, mh->m, err) != 0) {
+        std::fprintf(stderr, "rt_mesh_save_dae: %s\n", err.c_str());
+        return RT_ERR_INVALID_ARG;
+    }
+    return RT_OK;
+}
+
 int rt_mesh_gen_cornell(rt_mesh* mh) {
     if (!mh) return RT_ERR_INVALID_ARG;
     rtamd::gen_cornell(mh->m);

@@ -41,6 +41,9 @@ rt_material default_material();              // Material() (Mesh.h:37-41)
 rt_material diffuse_material(float r, float g, float b);
 
 int load_obj(const std::string& path, Mesh& m, std::string& err);
+// ColladaLoader::load + Mesh::init(ColladaLoader&) (collada.cpp); save_dae writes that subset.
+int load_dae(const std::string& path, Mesh& m, std::string& err);
+int save_dae(const std::string& path, const Mesh& m, std::string& err);
 void gen_cornell(Mesh& m);
 void gen_torus_knot(Mesh& m, int nu, int nv);
 void gen_heightfield(Mesh& m, int nx, int nz, float amplitude, uint32_t seed, float x0, float x1, float z0,

@@ -82,6 +82,7 @@ ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt
                "rt_tiling_pixels", "rt_last_timing", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
+                "rt_mesh_load_dae", "rt_mesh_save_dae",
                 "rt_mesh_gen_cornell", "rt_mesh_gen_torus_knot", "rt_mesh_gen_heightfield", "rt_mesh_gen_random",
                 "rt_mesh_append_grid", "rt_bvh_build", "rt_bvh_build_sbvh", "rt_bvh_view_get", "rt_bvh_destroy", "rt_bvh_save",
                 "rt_bvh_load", "rt_camera_params"]
@@ -126,6 +127,8 @@ def lib() -> C.CDLL:
             "rt_mesh_gen_heightfield": (C.c_int, [vp, i32, i32, f32, u32, f32, f32, f32, f32]),
             "rt_mesh_gen_random": (C.c_int, [vp, i32, f32, f32, u32]),
             "rt_mesh_append_grid": (C.c_int, [vp, vp, i32, i32, f32, f32, f32]),
+            "rt_mesh_load_dae": (C.c_int, [vp, C.c_char_p]),
+            "rt_mesh_save_dae": (C.c_int, [vp, C.c_char_p]),
             "rt_bvh_build": (C.c_int, [vp, i32, i32, C.POINTER(vp)]),
             "rt_bvh_build_sbvh": (C.c_int, [vp, i32, C.POINTER(vp)]),
             "rt_bvh_view_get": (C.c_int, [vp, C.POINTER(rt_bvh_view)]),
@@ -240,6 +243,15 @@ class Mesh:
     @classmethod
     def load_obj(cls, path: str) -> "Mesh":
         m = cls(); _check(lib().rt_mesh_load_obj(m._h, path.encode())); return m
+
+    @classmethod
+    def load_dae(cls, path: str) -> "Mesh":
+        """ColladaLoader::load + Mesh::init(ColladaLoader&) (ColladaLoader.cpp:13-593, Mesh.cpp:10-78)."""
+        m = cls(); _check(lib().rt_mesh_load_dae(m._h, path.encode())); return m
+
+    def save_dae(self, path: str) -> None:
+        """Writes the Collada subset load_dae (and the reference loader) reads."""
+        _check(lib().rt_mesh_save_dae(self._h, path.encode()))
 
     @classmethod
     def from_arrays(cls, vertices, indices, normals=None, normals_indices=None, materials=None,

@@ -120,7 +120,13 @@ def fixtures():
     fx["single_tri_rootleaf"] = _scene_dict(one, one.build_bvh(), 64, 64)
     fx["overflow_comb"] = _overflow_scene()
     fx["bad_node"] = _bad_node_scene()
+    m = rtamd.Mesh.random(4000, 100.0, 12.0, 3)   # long triangles: spatial splits, duplicated refs
+    fx["rand4k_sbvh"] = _scene_dict(m, m.build_sbvh(), 128, 128)
     if os.path.isdir(REF_DATA):
+        # the reference application's own scene: data/collada/cubes2.DAE through the
+        # Collada path and the spatial-split BVH (RayTracer.cpp's startup)
+        m = rtamd.Mesh.load_dae(os.path.join(REF_DATA, "collada", "cubes2.DAE"))
+        fx["cubes2_dae"] = _scene_dict(m, m.build_sbvh(), 256, 192)
         m = rtamd.Mesh.load_obj(os.path.join(REF_DATA, "models", "cubes2.obj"))
         fx["cubes2_obj"] = _scene_dict(m, m.build_bvh(), 256, 192)
         m = rtamd.Mesh.load_obj(os.path.join(REF_DATA, "sphere.obj"))
@@ -128,9 +134,11 @@ def fixtures():
     return fx
 
 
-def main(phase: str):
+def main(phase: str, only=()):
     if phase == "inputs":
         for name, d in fixtures().items():
+            if only and name not in only:
+                continue
             np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **d)
             print("wrote", name, int(d["indices"].size // 3), "tris", int(d["w"]), "x", int(d["h"]))
     elif phase == "reference":
@@ -140,6 +148,8 @@ def main(phase: str):
         print("OpenCL GPU devices:", ref_ocl.device_count())
         for fn in sorted(os.listdir(HERE)):
             if not fn.endswith(".npz") or fn.endswith(".ref.npz"):
+                continue
+            if only and fn[:-4] not in only:
                 continue
             d = dict(np.load(os.path.join(HERE, fn)))
             w, h = int(d["w"]), int(d["h"])
@@ -157,8 +167,8 @@ def main(phase: str):
             np.savez_compressed(os.path.join(HERE, name), **d)
             print("merged", name)
     else:
-        raise SystemExit("usage: make_golden.py inputs|reference|merge")
+        raise SystemExit("usage: make_golden.py inputs|reference|merge [fixture ...]")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "inputs")
+    main(sys.argv[1] if len(sys.argv) > 1 else "inputs", tuple(sys.argv[2:]))
