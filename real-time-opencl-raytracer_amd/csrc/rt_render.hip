@@ -178,7 +178,12 @@ struct Stack {
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // per-frame timing events, a ring over the last kRing frames:
+    // e[0]/e[1] around all kernels of the frame, e[2]/e[3] around the main render kernel
+    struct FrameEv { hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr}; bool has_k = false; };
+    static constexpr int kRing = 64;
+    FrameEv ring[kRing];
+    uint64_t frames = 0;
     float4* d_wnodes = nullptr;
     float4* d_tris = nullptr;
     float4* d_shade = nullptr;
@@ -308,7 +313,7 @@ int rt_create(int device, rt_ctx** out) {
     rt_ctx* c = new rt_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+
         hipMalloc((void**)&c->d_overflow, sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(c->d_overflow, 0, sizeof(unsigned long long)) != hipSuccess) {
         delete c;
@@ -333,8 +338,9 @@ int rt_destroy(rt_ctx* c) {
                     (void*)c->d_pstack, (void*)c->d_defer, (void*)c->d_order, (void*)c->d_wt,
                     (void*)c->d_cost, (void*)c->d_lpt})
         if (p) (void)hipFree(p);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (auto& f : c->ring)
+        for (hipEvent_t& e : f.e)
+            if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -556,6 +562,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.wave_times = nullptr;
 
     const bool hw = (flags & RT_FLAG_HW_MATH) != 0;
+    rt_ctx::FrameEv& E = c->ring[c->frames % rt_ctx::kRing];
+    for (hipEvent_t& e : E.e)
+        if (!e) HIPC(c, hipEventCreate(&e));
+    E.has_k = false;
     if (!(flags & RT_FLAG_WAVEFRONT) || depth == 0) {
         if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
         O.gstack = c->d_gstack;
@@ -602,29 +612,31 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         const bool fast_kernel = S.fast_div != 0 && S.clean != 0;
         const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
         const int ax = aux ? 1 : 0;
-        HIPC(c, hipEventRecord(c->ev0, s));
+        HIPC(c, hipEventRecord(E.e[0], s));
         if (lpt) {
             hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt,
                                F.num_blocks);
             F.tile_order = c->d_lpt;
         }
         if (F.tile_cost) c->cost_ready = true;
+        if (fast_kernel) HIPC(c, hipMemsetAsync(c->d_defer, 0, 16, s));
+        HIPC(c, hipEventRecord(E.e[2], s));
         if (fast_kernel) {
-            HIPC(c, hipMemsetAsync(c->d_defer, 0, 16, s));
-            if (hw) {
-                hipLaunchKernelGGL(rtk_hw::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
-                hipLaunchKernelGGL(rtk_hw::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
-            } else {
-                hipLaunchKernelGGL(rtk_strict::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
-                hipLaunchKernelGGL(rtk_strict::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
-            }
+            if (hw) hipLaunchKernelGGL(rtk_hw::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
+            else hipLaunchKernelGGL(rtk_strict::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
         } else if (hw) {
             hipLaunchKernelGGL(rtk_hw::render_kernel<false>, grid, block, 0, s, S, F, O, ax);
         } else {
             hipLaunchKernelGGL(rtk_strict::render_kernel<false>, grid, block, 0, s, S, F, O, ax);
         }
+        HIPC(c, hipEventRecord(E.e[3], s));
+        E.has_k = true;
+        if (fast_kernel) {  // the (normally empty) list of pixels the fast kernel handed back
+            if (hw) hipLaunchKernelGGL(rtk_hw::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
+            else hipLaunchKernelGGL(rtk_strict::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
+        }
         HIPC(c, hipGetLastError());
-        HIPC(c, hipEventRecord(c->ev1, s));
+        HIPC(c, hipEventRecord(E.e[1], s));
 #if RTK_WAVE_TIMES
         if (O.wave_times) {
             HIPC(c, hipStreamSynchronize(s));
@@ -637,6 +649,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         }
 #endif
     } else {
+        E.has_k = false;
         // persistent grids: blocks per CU from the occupancy query, x CUs, multiple of 8 (partitions)
         const int mi = hw ? 1 : 0;
         if (!c->grid_k1[mi]) {
@@ -673,7 +686,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         const uint32_t tiles = ((w + 7) / 8) * ((F.local_rows + 7) / 8);
         Pp.n_items = tiles * 64;
         Pp.part_items = ((tiles + 7) / 8) * 64;
-        HIPC(c, hipEventRecord(c->ev0, s));
+        HIPC(c, hipEventRecord(E.e[0], s));
         HIPC(c, hipMemsetAsync(c->d_heads, 0, (size_t)2 * depth * 16 * sizeof(uint32_t), s));
         for (int b = 0; b < depth; ++b) {
             Pp.bounce = b;
@@ -688,9 +701,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             }
             HIPC(c, hipGetLastError());
         }
-        HIPC(c, hipEventRecord(c->ev1, s));
+        HIPC(c, hipEventRecord(E.e[1], s));
     }
     c->timing_valid = true;
+    ++c->frames;
     return RT_OK;
 }
 
@@ -722,14 +736,50 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
     return RT_OK;
 }
 
+static int frame_times(rt_ctx* c, uint64_t f, float& total, float& kernel) {
+    rt_ctx::FrameEv& E = c->ring[f % rt_ctx::kRing];
+    HIPC(c, hipEventSynchronize(E.e[1]));
+    HIPC(c, hipEventElapsedTime(&total, E.e[0], E.e[1]));
+    kernel = total;
+    if (E.has_k) HIPC(c, hipEventElapsedTime(&kernel, E.e[2], E.e[3]));
+    return RT_OK;
+}
+
 int rt_last_timing(rt_ctx* c, float* total_ms, float* traverse_ms) {
     if (!c || !total_ms) return RT_ERR_INVALID_ARG;
-    if (!c->timing_valid) return set_err(c, "rt_last_timing: nothing rendered", RT_ERR_NO_SCENE);
-    HIPC(c, hipEventSynchronize(c->ev1));
-    float ms = 0;
-    HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    *total_ms = ms;
-    if (traverse_ms) *traverse_ms = ms;
+    if (!c->timing_valid || c->frames == 0) return set_err(c, "rt_last_timing: nothing rendered", RT_ERR_NO_SCENE);
+    float t = 0, k = 0;
+    int rc;
+    if ((rc = frame_times(c, c->frames - 1, t, k))) return rc;
+    *total_ms = t;
+    if (traverse_ms) *traverse_ms = k;
+    return RT_OK;
+}
+
+int rt_timing_average(rt_ctx* c, int32_t n, float* total_ms, float* traverse_ms) {
+    if (!c || !total_ms || n < 1) return RT_ERR_INVALID_ARG;
+    if (c->frames == 0) return set_err(c, "rt_timing_average: nothing rendered", RT_ERR_NO_SCENE);
+    const uint64_t m = std::min<uint64_t>({(uint64_t)n, c->frames, (uint64_t)rt_ctx::kRing});
+    double st = 0, sk = 0;
+    for (uint64_t i = 0; i < m; ++i) {
+        float t = 0, k = 0;
+        int rc;
+        if ((rc = frame_times(c, c->frames - 1 - i, t, k))) return rc;
+        st += t;
+        sk += k;
+    }
+    *total_ms = (float)(st / (double)m);
+    if (traverse_ms) *traverse_ms = (float)(sk / (double)m);
+    return RT_OK;
+}
+
+int rt_last_deferred(rt_ctx* c, uint32_t* count) {
+    if (!c || !count) return RT_ERR_INVALID_ARG;
+    *count = 0;
+    if (!c->d_defer) return RT_OK;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipDeviceSynchronize());
+    HIPC(c, hipMemcpy(count, c->d_defer, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

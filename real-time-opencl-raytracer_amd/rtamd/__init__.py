@@ -79,7 +79,7 @@ class rt_bvh_view(C.Structure):
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
 ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_device",
-               "rt_tiling_pixels", "rt_last_timing", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_tiling_pixels", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
@@ -113,6 +113,8 @@ def lib() -> C.CDLL:
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
             "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
+            "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
+            "rt_last_deferred": (C.c_int, [vp, C.POINTER(u32)]),
             "rt_overflow_count": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
             "rt_destroy": (C.c_int, [vp]),
             "rt_last_error": (C.c_char_p, [vp]),
@@ -396,9 +398,28 @@ class Renderer:
                                       C.c_void_p(d_out_ptr), ax, C.c_void_p(stream or None)), self._h)
 
     def last_kernel_ms(self) -> float:
+        """All kernels of the last frame (ms, HIP events on the launch stream)."""
         t = C.c_float()
         _check(lib().rt_last_timing(self._h, C.byref(t), None), self._h)
         return t.value
+
+    def last_timing(self):
+        """(frame kernels ms, fused render kernel alone ms) of the last frame."""
+        t, k = C.c_float(), C.c_float()
+        _check(lib().rt_last_timing(self._h, C.byref(t), C.byref(k)), self._h)
+        return t.value, k.value
+
+    def timing_average(self, n: int):
+        """(frame kernels ms, fused render kernel ms) averaged over the last n frames (n <= 64)."""
+        t, k = C.c_float(), C.c_float()
+        _check(lib().rt_timing_average(self._h, n, C.byref(t), C.byref(k)), self._h)
+        return t.value, k.value
+
+    def last_deferred(self) -> int:
+        """Pixels the fast kernel handed back to the general kernel in the last frame."""
+        v = C.c_uint32()
+        _check(lib().rt_last_deferred(self._h, C.byref(v)), self._h)
+        return v.value
 
     def overflow_count(self) -> int:
         v = C.c_uint64()

@@ -162,10 +162,11 @@ def test_tiny_coordinates_fall_back_to_division(renderer):
     _compare(gpu, ref, "tiny coordinates")
 
 
-def test_zero_direction_component_pixels_are_handed_back(renderer):
-    """An axis-aligned camera gives rays with a direction component exactly 0 (outside
-    the fast quotient's domain): the fast kernel hands those pixels to the general
-    kernel (render_list_kernel); the frame must still match the oracle."""
+def test_zero_direction_component_pixels(renderer):
+    """An axis-aligned camera gives rays with a direction component exactly 0: the fast
+    kernel's quotient takes a * (1/d) = +-inf / NaN as the IEEE quotient there (pk_xdiv's
+    select) instead of handing the pixel to the general kernel; the frame must match the
+    oracle bit for bit."""
     import rtamd
     d = load_golden("knot16k")
     s = _scene(d)
@@ -185,6 +186,7 @@ def test_zero_direction_component_pixels_are_handed_back(renderer):
     renderer.set_params(p)
     gpu = renderer.render(w, h, depth=3, aux=True)
     _compare(gpu, _oracle(d, 3, w=w, h=h, params=p), "axis-aligned camera")
+    assert renderer.last_deferred() == 0
 
 
 @pytest.mark.parametrize("name", golden_names())
