@@ -1,0 +1,61 @@
+"""Copies the judged profile artefacts of scripts/profile_c3.sh into profiles/<round>/
+and writes profiles/pmc_<config>.json (HBM bytes per render-kernel launch).
+
+FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B/lane reads,
+MI355X_MICROARCH.md HBM section); FETCH_SIZE / WRITE_SIZE are in kB = 1024 B.
+
+    python scripts/profile_summary.py r01 [c3]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "render_kernel<true>"
+
+
+def counter(d, name):
+    f = glob.glob(os.path.join(ROOT, "gpurun_out", d, "**", "*counter_collection.csv"), recursive=True)[0]
+    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if KERNEL in r["Kernel_Name"]
+         and r["Counter_Name"] == name]
+    return statistics.median(v), len(v), f
+
+
+def main():
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
+    out = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(out, exist_ok=True)
+    stats = glob.glob(os.path.join(ROOT, "gpurun_out", "prof_trace", "**", "*kernel_stats.csv"), recursive=True)[0]
+    shutil.copy(stats, os.path.join(out, f"{cfg}_kernel_stats.csv"))
+    avg_ns = None
+    for r in csv.DictReader(open(stats)):
+        if KERNEL in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+    fetch, nf, ff = counter("prof_fetch", "FETCH_SIZE")
+    write, nw, fw = counter("prof_write", "WRITE_SIZE")
+    shutil.copy(ff, os.path.join(out, f"{cfg}_pmc_fetch.csv"))
+    shutil.copy(fw, os.path.join(out, f"{cfg}_pmc_write.csv"))
+    for log in ("prof_bench.log", "prof_trace.log"):
+        p = os.path.join(ROOT, "gpurun_out", log)
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(out, f"{cfg}_{log.replace('prof_', '')}"))
+    res = {
+        "config": cfg, "kernel": "rtk_strict::render_kernel<true>", "round": rnd,
+        "rocprof_avg_kernel_us": None if avg_ns is None else round(avg_ns / 1e3, 2),
+        "FETCH_SIZE_kB_median": fetch, "WRITE_SIZE_kB_median": write, "dispatches": [nf, nw],
+        "correction": "FETCH_SIZE x2 (gfx950 reports half the bytes of 16B/lane reads, MI355X_MICROARCH.md HBM); "
+                      "kB = 1024 B",
+        "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
+        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --config " + cfg,
+    }
+    json.dump(res, open(os.path.join(ROOT, "profiles", f"pmc_{cfg}.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
