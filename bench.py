@@ -258,7 +258,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_ray": round(bpr, 1), "kernel_ms": round(kernel_ms_avg, 4),
-                     "frame_kernels_ms": round(frame_ms_avg, 4), "kernel": "rtk_strict::render_kernel<true>"},
+                     "frame_kernels_ms": round(frame_ms_avg, 4),
+                     "kernel": ("rtk_strict::first_bounce_kernel<true>" if depth == 1 or (flags & 8)
+                                else "rtk_strict::render_kernel<true>")},
         "cpu_baseline": cpu,
     }
     print(json.dumps(res))

@@ -72,9 +72,12 @@ enum {
                                 device-library functions the reference kernel links
                                 (v_rsq_f32, __ocml_pow_f32) instead of the S_strict
                                 CPU-reproducible ones */
-    RT_FLAG_WAVEFRONT = 8u,  /* per-bounce persistent pipeline (closest-hit trace kernel, then shade +
-                                shadow-trace kernel, ballot refill of idle lanes) instead of the default
-                                fused one-lane-per-pixel kernel; bit-identical, currently slower */
+    RT_FLAG_WAVEFRONT = 8u,  /* wavefront mode: bounce 0 over screen tiles, then one
+                                launch per further bounce over a compacted queue of the rays still in
+                                flight, instead of the fused one-lane-per-pixel kernel; bit-identical.
+                                Depth-1 frames always run as that first launch alone. */
+    RT_FLAG_WF_SORT = 32u,   /* with RT_FLAG_WAVEFRONT: sort each bounce's queue by (direction octant,
+                                leaf position of the triangle the ray leaves) before tracing it */
     RT_FLAG_EXACT_DIV = 4u,  /* force the IEEE-division slab test (volumeRender.cl:614-615) instead of
                                 the bit-identical 3-op fast quotient; for A/B only */
     RT_FLAG_STATIC_ORDER = 16u /* fused kernel: keep the static XCD-dealt block order instead of the

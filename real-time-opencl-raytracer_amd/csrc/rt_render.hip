@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "rt_abi.h"
+#include <hipcub/hipcub.hpp>
 
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 20
@@ -102,19 +103,22 @@ struct Frame {
     uint32_t* tile_cost;          // [num_blocks] per-tile wall time of this frame (adaptive order), or null
 };
 
-// Pipelined path state (per local pixel) and work partitions.
-struct Pipe {
-    int2* hit_t;          // {closest hit id, t bits} of the current bounce
-    int* state;           // kAlive | ray_depth while the pixel still traces
-    float4* acc;          // colour.xyz, shadow_sum carried between bounces
-    float4* rays;         // [2] reflection ray {o, d} for the next bounce
-    uint32_t* heads;      // [2 * depth][16] partition fetch counters (zeroed per frame)
-    uint64_t n_slots;     // persistent lanes (global overflow-stack stride)
-    uint32_t n_items;     // 8x8-tile items covering the local frame
-    uint32_t part_items;  // items per partition (multiple of 64)
+// Wavefront path (rt_kernel_body.inc): a ray in flight between bounces --
+// {pix, o.xyz}, {d.xyz, shadow_sum}, {colour.xyz, 3 * triangle it leaves from}.
+struct QRay {
+    float4 a, b, c;
+};
+struct WQ {
+    const QRay* in;           // this bounce's rays, or the handed-back rays of this bounce
+    const uint32_t* in_count;
+    const uint32_t* perm;     // optional order of `in` (sorted), or null
+    QRay* out;                // next bounce's rays
+    uint32_t* out_count;
+    QRay* slow;               // rays of this bounce the fast code hands back
+    uint32_t* slow_count;
+    uint32_t* fetch;          // dynamic work counter of this launch
     int bounce;
 };
-constexpr int kAlive = 0x40000000;
 
 struct Outputs {
     uint32_t* out;
@@ -201,12 +205,12 @@ struct rt_ctx {
     uint32_t* d_gstack = nullptr; size_t gstack_cap = 0;   // in pixels
     unsigned long long* d_overflow = nullptr;
     // pipelined path buffers (per local pixel) + persistent grid sizes
-    int2* d_hit_t = nullptr; size_t hit_t_cap = 0;
-    int* d_state = nullptr; size_t state_cap = 0;
-    float4* d_acc = nullptr; size_t acc_cap = 0;
-    float4* d_rays = nullptr; size_t rays_cap = 0;
-    uint32_t* d_heads = nullptr; size_t heads_cap = 0;
-    uint32_t* d_pstack = nullptr; size_t pstack_cap = 0;
+    float4* d_wq[2] = {nullptr, nullptr}; size_t wq_cap[2] = {0, 0};   // wavefront ray queues (ping-pong)
+    float4* d_wslow = nullptr; size_t wslow_cap = 0;                    // rays handed to the general code
+    uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // per-bounce counters
+    uint32_t* d_sort[4] = {nullptr, nullptr, nullptr, nullptr}; size_t sort_cap[4] = {0, 0, 0, 0};
+    uint8_t* d_sort_tmp = nullptr; size_t sort_tmp_cap = 0;
+    uint32_t* d_rank = nullptr;                                         // triangle -> first leaf position
     uint32_t* d_wt = nullptr; size_t wt_cap = 0;             // RTK_WAVE_TIMES
     uint32_t* d_defer = nullptr; size_t defer_cap = 0;       // [4 + P]: count, then deferred pixels
     uint32_t* d_order = nullptr; size_t order_cap = 0;        // tile order table for the fused kernel
@@ -215,7 +219,7 @@ struct rt_ctx {
     uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;            //   and the longest-first order built from them
     uint64_t cost_key = 0; bool cost_ready = false;
     uint32_t scene_gen = 0;                                   // bumped by every upload
-    int grid_k1[2] = {0, 0}, grid_k2[2] = {0, 0};   // [strict, hw]
+    int wf_grid[2] = {0, 0};   // persistent wavefront grid [strict, hw]
     float last_ms = 0.0f;
     bool timing_valid = false;
     std::string err;
@@ -245,12 +249,23 @@ static int ensure(rt_ctx* c, T*& p, size_t& cap, size_t n) {
     return RT_OK;
 }
 
+// Per-bounce ray sort of the wavefront path (32-bit keys, 32-bit payloads).
+static hipError_t rtk_sort_temp_bytes(int n, size_t& bytes) {
+    return hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, n);
+}
+static hipError_t rtk_sort_pairs(uint8_t* tmp, size_t bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                                 uint32_t* vout, int n, hipStream_t s) {
+    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, 32, s);
+}
+
 static void free_scene(rt_ctx* c) {
     if (c->d_wnodes) (void)hipFree(c->d_wnodes);
     if (c->d_tris) (void)hipFree(c->d_tris);
     if (c->d_shade) (void)hipFree(c->d_shade);
     if (c->d_leaf) (void)hipFree(c->d_leaf);
-    c->d_wnodes = nullptr; c->d_tris = nullptr; c->d_shade = nullptr; c->d_leaf = nullptr;
+    if (c->d_rank) (void)hipFree(c->d_rank);
+    c->d_wnodes = nullptr; c->d_tris = nullptr; c->d_shade = nullptr; c->d_leaf = nullptr; c->d_rank = nullptr;
     c->have_scene = false;
 }
 
@@ -334,8 +349,9 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_gstack) (void)hipFree(c->d_gstack);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
-    for (void* p : {(void*)c->d_hit_t, (void*)c->d_state, (void*)c->d_acc, (void*)c->d_rays, (void*)c->d_heads,
-                    (void*)c->d_pstack, (void*)c->d_defer, (void*)c->d_order, (void*)c->d_wt,
+    for (void* p : {(void*)c->d_wq[0], (void*)c->d_wq[1], (void*)c->d_wslow, (void*)c->d_wcnt, (void*)c->d_sort[0],
+                    (void*)c->d_sort[1], (void*)c->d_sort[2], (void*)c->d_sort[3], (void*)c->d_sort_tmp,
+                    (void*)c->d_defer, (void*)c->d_order, (void*)c->d_wt,
                     (void*)c->d_cost, (void*)c->d_lpt})
         if (p) (void)hipFree(p);
     for (auto& f : c->ring)
@@ -479,6 +495,12 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         HIPC(c, hipMalloc((void**)&c->d_leaf, leaf_table.size() * sizeof(int2)));
         HIPC(c, hipMemcpy(c->d_wnodes, wn.data(), wn.size() * sizeof(float4), hipMemcpyHostToDevice));
         HIPC(c, hipMemcpy(c->d_tris, tr.data(), tr.size() * sizeof(float4), hipMemcpyHostToDevice));
+        {   // triangle -> position of its first reference in leaf order (wavefront sort keys)
+            std::vector<uint32_t> rank((size_t)std::max(ntri, 1), 0x1FFFFFFEu);
+            for (int32_t i = nref - 1; i >= 0; --i) rank[(size_t)(refs[i] / 3)] = (uint32_t)i;
+            HIPC(c, hipMalloc((void**)&c->d_rank, rank.size() * sizeof(uint32_t)));
+            HIPC(c, hipMemcpy(c->d_rank, rank.data(), rank.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
         HIPC(c, hipMemcpy(c->d_shade, sh.data(), sh.size() * sizeof(float4), hipMemcpyHostToDevice));
         HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
         c->root = ref_of[0];
@@ -566,59 +588,65 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     for (hipEvent_t& e : E.e)
         if (!e) HIPC(c, hipEventCreate(&e));
     E.has_k = false;
-    if (!(flags & RT_FLAG_WAVEFRONT) || depth == 0) {
-        if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
-        O.gstack = c->d_gstack;
-        if ((rc = ensure(c, c->d_defer, c->defer_cap, (size_t)npix + 4))) return rc;
-        O.defer = c->d_defer + 4;
-        O.defer_count = c->d_defer;
+    // depth 1 always takes the wavefront route: it is then one first_bounce_kernel launch,
+    // the fused kernel specialised to a single bounce
+    const bool wavefront = ((flags & RT_FLAG_WAVEFRONT) && depth > 0) || depth == 1;
+
+    if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
+    O.gstack = c->d_gstack;
+    if ((rc = ensure(c, c->d_defer, c->defer_cap, (size_t)npix + 4))) return rc;
+    O.defer = c->d_defer + 4;
+    O.defer_count = c->d_defer;
 #if RTK_WAVE_TIMES
-        if (std::getenv("RTAMD_WAVE_TIMES")) {
-            if ((rc = ensure(c, c->d_wt, c->wt_cap, (size_t)npix * 4))) return rc;
-            HIPC(c, hipMemsetAsync(c->d_wt, 0, (size_t)npix * 16, s));
-            O.wave_times = c->d_wt;
-        }
+    if (std::getenv("RTAMD_WAVE_TIMES")) {
+        if ((rc = ensure(c, c->d_wt, c->wt_cap, (size_t)npix * 4))) return rc;
+        HIPC(c, hipMemsetAsync(c->d_wt, 0, (size_t)npix * 16, s));
+        O.wave_times = c->d_wt;
+    }
 #endif
-        F.tile_order = nullptr;
-        const int pol = tile_order_policy();
-        if (pol != 0) {
-            if (c->order_policy != pol || c->order_tx != F.tiles_x || c->order_ty != F.tiles_y) {
-                const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y, pol);
-                if ((rc = ensure(c, c->d_order, c->order_cap, tab.size()))) return rc;
-                HIPC(c, hipMemcpy(c->d_order, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
-                c->order_policy = pol;
-                c->order_tx = F.tiles_x;
-                c->order_ty = F.tiles_y;
-            }
-            F.tile_order = c->d_order;
+    // static block order (in-kernel XCD chunk dealing, or a host-built table)
+    F.tile_order = nullptr;
+    const int pol = tile_order_policy();
+    if (pol != 0) {
+        if (c->order_policy != pol || c->order_tx != F.tiles_x || c->order_ty != F.tiles_y) {
+            const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y, pol);
+            if ((rc = ensure(c, c->d_order, c->order_cap, tab.size()))) return rc;
+            HIPC(c, hipMemcpy(c->d_order, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+            c->order_policy = pol;
+            c->order_tx = F.tiles_x;
+            c->order_ty = F.tiles_y;
         }
-        // Adaptive longest-first order (tile_order_kernel) from the previous frame of
-        // the same geometry; the first frame runs the static order and measures.
-        F.tile_cost = nullptr;
-        bool lpt = false;
-        if (!(flags & RT_FLAG_STATIC_ORDER)) {
-            if ((rc = ensure(c, c->d_cost, c->cost_cap, F.num_blocks))) return rc;
-            if ((rc = ensure(c, c->d_lpt, c->lpt_cap, F.num_blocks))) return rc;
-            const uint64_t key = ((uint64_t)F.tiles_x << 48) ^ ((uint64_t)F.tiles_y << 32) ^ F.local_rows ^
-                                 ((uint64_t)c->scene_gen << 20);
-            if (key != c->cost_key) {
-                HIPC(c, hipMemsetAsync(c->d_cost, 0, (size_t)F.num_blocks * 4, s));
-                c->cost_key = key;
-                c->cost_ready = false;
-            }
-            lpt = c->cost_ready;
-            F.tile_cost = c->d_cost;
+        F.tile_order = c->d_order;
+    }
+    // Adaptive longest-first order (tile_order_kernel) from the previous frame of
+    // the same geometry; the first frame runs the static order and measures.
+    F.tile_cost = nullptr;
+    bool lpt = false;
+    if (!(flags & RT_FLAG_STATIC_ORDER)) {
+        if ((rc = ensure(c, c->d_cost, c->cost_cap, F.num_blocks))) return rc;
+        if ((rc = ensure(c, c->d_lpt, c->lpt_cap, F.num_blocks))) return rc;
+        const uint64_t key = ((uint64_t)F.tiles_x << 48) ^ ((uint64_t)F.tiles_y << 32) ^ F.local_rows ^
+                             ((uint64_t)c->scene_gen << 20) ^ (wavefront ? (1ull << 63) : 0ull);
+        if (key != c->cost_key) {
+            HIPC(c, hipMemsetAsync(c->d_cost, 0, (size_t)F.num_blocks * 4, s));
+            c->cost_key = key;
+            c->cost_ready = false;
         }
-        const bool fast_kernel = S.fast_div != 0 && S.clean != 0;
-        const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
-        const int ax = aux ? 1 : 0;
-        HIPC(c, hipEventRecord(E.e[0], s));
-        if (lpt) {
-            hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt,
-                               F.num_blocks);
-            F.tile_order = c->d_lpt;
-        }
-        if (F.tile_cost) c->cost_ready = true;
+        lpt = c->cost_ready;
+        F.tile_cost = c->d_cost;
+    }
+    const bool fast_kernel = S.fast_div != 0 && S.clean != 0;
+    const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
+    const int ax = aux ? 1 : 0;
+    HIPC(c, hipEventRecord(E.e[0], s));
+    if (lpt) {
+        hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt,
+                           F.num_blocks);
+        F.tile_order = c->d_lpt;
+    }
+    if (F.tile_cost) c->cost_ready = true;
+
+    if (!wavefront) {
         if (fast_kernel) HIPC(c, hipMemsetAsync(c->d_defer, 0, 16, s));
         HIPC(c, hipEventRecord(E.e[2], s));
         if (fast_kernel) {
@@ -637,70 +665,99 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         }
         HIPC(c, hipGetLastError());
         HIPC(c, hipEventRecord(E.e[1], s));
-#if RTK_WAVE_TIMES
-        if (O.wave_times) {
-            HIPC(c, hipStreamSynchronize(s));
-            std::vector<uint32_t> wt((size_t)npix * 4);
-            HIPC(c, hipMemcpy(wt.data(), O.wave_times, wt.size() * 4, hipMemcpyDeviceToHost));
-            if (FILE* f = std::fopen(std::getenv("RTAMD_WAVE_TIMES"), "wb")) {
-                std::fwrite(wt.data(), 4, wt.size(), f);
-                std::fclose(f);
-            }
-        }
-#endif
     } else {
-        E.has_k = false;
-        // persistent grids: blocks per CU from the occupancy query, x CUs, multiple of 8 (partitions)
+        // Wavefront: bounce 0 over tiles, then one persistent launch per further bounce
+        // over the queue of rays still in flight (+ the general code for handed-back rays).
         const int mi = hw ? 1 : 0;
-        if (!c->grid_k1[mi]) {
-            int cus = 0, b1 = 0, b2 = 0;
+        if (!c->wf_grid[mi]) {
+            int cus = 0, b1 = 0;
             HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-            if (hw) {
-                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_hw::trace_closest_kernel, 256, 0));
-                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, rtk_hw::shade_shadow_kernel, 256, 0));
+            if (hw) HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_hw::wf_bounce_kernel<true>, 256, 0));
+            else HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_strict::wf_bounce_kernel<true>, 256, 0));
+            c->wf_grid[mi] = std::max(8, std::max(b1, 1) * cus);
+        }
+        const size_t qcap = (size_t)npix * 3;  // float4 per QRay x 3
+        if (depth > 1 && (rc = ensure(c, c->d_wq[0], c->wq_cap[0], qcap))) return rc;
+        if (depth > 1 && (rc = ensure(c, c->d_wq[1], c->wq_cap[1], qcap))) return rc;
+        if ((rc = ensure(c, c->d_wslow, c->wslow_cap, qcap))) return rc;
+        if ((rc = ensure(c, c->d_wcnt, c->wcnt_cap, 8 * (RT_MAX_DEPTH + 1)))) return rc;
+        const bool sort = (flags & RT_FLAG_WF_SORT) && depth > 1 && c->d_rank;
+        if (sort) {
+            for (int i = 0; i < 4; ++i)
+                if ((rc = ensure(c, c->d_sort[i], c->sort_cap[i], (size_t)npix))) return rc;
+            size_t need = 0;
+            HIPC(c, rtk_sort_temp_bytes((int)npix, need));
+            if ((rc = ensure(c, c->d_sort_tmp, c->sort_tmp_cap, need))) return rc;
+        }
+        HIPC(c, hipMemsetAsync(c->d_wcnt, 0, 8 * (RT_MAX_DEPTH + 1) * sizeof(uint32_t), s));
+        // counters per bounce k: [8k+0] queue size of bounce k, [8k+1] slow size, [8k+2] fetch, [8k+3] slow fetch
+        auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)c->d_wq[k & 1] : (rtk::QRay*)nullptr; };
+        uint32_t* cnt = c->d_wcnt;
+        HIPC(c, hipEventRecord(E.e[2], s));
+        {
+            rtk::WQ W{};
+            W.out = qbuf(1);
+            W.out_count = cnt + 8 * 1 + 0;
+            W.slow = (rtk::QRay*)c->d_wslow;
+            W.slow_count = cnt + 8 * 0 + 1;
+            W.bounce = 0;
+            if (fast_kernel) {
+                if (hw) hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<true>, grid, block, 0, s, S, F, O, W, ax);
+                else hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<true>, grid, block, 0, s, S, F, O, W, ax);
+            } else if (hw) {
+                hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<false>, grid, block, 0, s, S, F, O, W, ax);
             } else {
-                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_strict::trace_closest_kernel, 256, 0));
-                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, rtk_strict::shade_shadow_kernel, 256, 0));
+                hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<false>, grid, block, 0, s, S, F, O, W, ax);
             }
-            c->grid_k1[mi] = std::max(8, (std::max(b1, 1) * cus) & ~7);
-            c->grid_k2[mi] = std::max(8, (std::max(b2, 1) * cus) & ~7);
         }
-        const int g1 = c->grid_k1[mi], g2 = c->grid_k2[mi];
-        const size_t slots = (size_t)std::max(g1, g2) * 256;
-        if ((rc = ensure(c, c->d_pstack, c->pstack_cap, slots * rtk::kGlobalStack))) return rc;
-        if ((rc = ensure(c, c->d_hit_t, c->hit_t_cap, (size_t)npix))) return rc;
-        if ((rc = ensure(c, c->d_state, c->state_cap, (size_t)npix))) return rc;
-        if (depth > 1) {
-            if ((rc = ensure(c, c->d_acc, c->acc_cap, (size_t)npix))) return rc;
-            if ((rc = ensure(c, c->d_rays, c->rays_cap, (size_t)npix * 2))) return rc;
-        }
-        if ((rc = ensure(c, c->d_heads, c->heads_cap, (size_t)2 * RT_MAX_DEPTH * 16))) return rc;
-        O.gstack = c->d_pstack;
-        rtk::Pipe Pp;
-        Pp.hit_t = c->d_hit_t;
-        Pp.state = c->d_state;
-        Pp.acc = c->d_acc;
-        Pp.rays = c->d_rays;
-        Pp.heads = c->d_heads;
-        Pp.n_slots = slots;
-        const uint32_t tiles = ((w + 7) / 8) * ((F.local_rows + 7) / 8);
-        Pp.n_items = tiles * 64;
-        Pp.part_items = ((tiles + 7) / 8) * 64;
-        HIPC(c, hipEventRecord(E.e[0], s));
-        HIPC(c, hipMemsetAsync(c->d_heads, 0, (size_t)2 * depth * 16 * sizeof(uint32_t), s));
-        for (int b = 0; b < depth; ++b) {
-            Pp.bounce = b;
-            if (hw) {
-                hipLaunchKernelGGL(rtk_hw::trace_closest_kernel, dim3(g1), dim3(256), 0, s, S, F, O, Pp, aux ? 1 : 0);
-                hipLaunchKernelGGL(rtk_hw::shade_shadow_kernel, dim3(g2), dim3(256), 0, s, S, F, O, Pp, aux ? 1 : 0);
-            } else {
-                hipLaunchKernelGGL(rtk_strict::trace_closest_kernel, dim3(g1), dim3(256), 0, s, S, F, O, Pp,
-                                   aux ? 1 : 0);
-                hipLaunchKernelGGL(rtk_strict::shade_shadow_kernel, dim3(g2), dim3(256), 0, s, S, F, O, Pp,
-                                   aux ? 1 : 0);
+        HIPC(c, hipEventRecord(E.e[3], s));
+        E.has_k = true;
+        for (int k = 0; k < depth; ++k) {
+            if (k > 0) {  // fast launch of bounce k over its queue
+                rtk::WQ W{};
+                W.in = qbuf(k);
+                W.in_count = cnt + 8 * k + 0;
+                W.perm = nullptr;
+                if (sort) {
+                    hipLaunchKernelGGL(rtk_strict::wf_key_kernel, dim3(1024), dim3(256), 0, s,
+                                       (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, c->d_sort[0],
+                                       c->d_sort[1], c->d_rank);
+                    HIPC(c, rtk_sort_pairs(c->d_sort_tmp, c->sort_tmp_cap, c->d_sort[0], c->d_sort[2], c->d_sort[1],
+                                           c->d_sort[3], (int)npix, s));
+                    W.perm = c->d_sort[3];
+                }
+                W.out = qbuf(k + 1);
+                W.out_count = cnt + 8 * (k + 1) + 0;
+                W.slow = (rtk::QRay*)c->d_wslow;
+                W.slow_count = cnt + 8 * k + 1;
+                W.fetch = cnt + 8 * k + 2;
+                W.bounce = k;
+                const dim3 pg(c->wf_grid[mi]);
+                if (fast_kernel) {
+                    if (hw) hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
+                    else hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
+                } else if (hw) {
+                    hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
+                } else {
+                    hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
+                }
             }
-            HIPC(c, hipGetLastError());
+            if (fast_kernel) {  // general code over the rays of bounce k the fast code handed back
+                rtk::WQ W{};
+                W.in = (rtk::QRay*)c->d_wslow;
+                W.in_count = cnt + 8 * k + 1;
+                W.perm = nullptr;
+                W.out = qbuf(k + 1);
+                W.out_count = cnt + 8 * (k + 1) + 0;
+                W.slow = nullptr;
+                W.slow_count = nullptr;
+                W.fetch = cnt + 8 * k + 3;
+                W.bounce = k;
+                if (hw) hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<false>, lgrid, dim3(256), 0, s, S, F, O, W, ax);
+                else hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<false>, lgrid, dim3(256), 0, s, S, F, O, W, ax);
+            }
         }
+        HIPC(c, hipGetLastError());
         HIPC(c, hipEventRecord(E.e[1], s));
     }
     c->timing_valid = true;

@@ -191,16 +191,21 @@ def test_zero_direction_component_pixels(renderer):
 
 @pytest.mark.parametrize("name", golden_names())
 @pytest.mark.parametrize("depth", [1, 3])
-def test_fused_and_pipelined_paths_agree(renderer, name, depth):
-    """The default fused kernel and RT_FLAG_WAVEFRONT (persistent per-bounce pipeline) give the same bits."""
+@pytest.mark.parametrize("sort", [False, True])
+def test_fused_and_wavefront_paths_agree(renderer, name, depth, sort):
+    """The default fused kernel and RT_FLAG_WAVEFRONT (one launch per bounce over a compacted
+    ray queue, optionally sorted per bounce) give the same bits, aux planes included."""
     import rtamd
     d = load_golden(name)
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     w, h = int(d["w"]), int(d["h"])
     fused = renderer.render(w, h, depth=depth, aux=True)
-    pipe = renderer.render(w, h, depth=depth, flags=rtamd.RT_FLAG_WAVEFRONT, aux=True)
-    _compare(pipe, fused, f"{name} depth={depth} pipelined-vs-fused")
+    flags = rtamd.RT_FLAG_WAVEFRONT | (rtamd.RT_FLAG_WF_SORT if sort else 0)
+    wf = renderer.render(w, h, depth=depth, flags=flags, aux=True)
+    _compare(wf, fused, f"{name} depth={depth} sort={sort} wavefront-vs-fused")
+    wf2 = renderer.render(w, h, depth=depth, flags=flags, aux=True)   # longest-first block order
+    _compare(wf2, fused, f"{name} depth={depth} sort={sort} wavefront-vs-fused (adaptive order)")
 
 
 @pytest.mark.parametrize("name", ["hf40k", "knot16k"])
