@@ -760,6 +760,17 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         HIPC(c, hipGetLastError());
         HIPC(c, hipEventRecord(E.e[1], s));
     }
+#if RTK_WAVE_TIMES
+    if (O.wave_times) {
+        HIPC(c, hipStreamSynchronize(s));
+        std::vector<uint32_t> wt((size_t)npix * 4);
+        HIPC(c, hipMemcpy(wt.data(), O.wave_times, wt.size() * 4, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(std::getenv("RTAMD_WAVE_TIMES"), "wb")) {
+            std::fwrite(wt.data(), 4, wt.size(), f);
+            std::fclose(f);
+        }
+    }
+#endif
     c->timing_valid = true;
     ++c->frames;
     return RT_OK;
