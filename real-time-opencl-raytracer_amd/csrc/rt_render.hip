@@ -66,6 +66,9 @@
 #ifndef RTK_PROBE_EXTRA_LOAD
 #define RTK_PROBE_EXTRA_LOAD 0
 #endif
+#ifndef RTK_PERSISTENT
+#define RTK_PERSISTENT 0   // first_bounce_kernel: persistent waves over a tile counter (A/B: slower)
+#endif
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
 #endif
@@ -101,6 +104,9 @@ struct Frame {
     uint32_t tiles_x, tiles_y, num_blocks;
     const uint32_t* tile_order;   // [num_blocks] block -> tile, or null (in-kernel chunk dealing)
     uint32_t* tile_cost;          // [num_blocks] per-tile wall time of this frame (adaptive order), or null
+    // persistent first-bounce kernel: 8x8 tiles taken from a counter (null = one block per tile group)
+    uint32_t* work_counter;
+    uint32_t tiles8_x, num_tiles8;
 };
 
 // Wavefront path (rt_kernel_body.inc): a ray in flight between bounces --
@@ -220,6 +226,7 @@ struct rt_ctx {
     uint64_t cost_key = 0; bool cost_ready = false;
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[2] = {0, 0};   // persistent wavefront grid [strict, hw]
+    int fb_grid[2] = {0, 0};   // persistent first_bounce_kernel grid [strict, hw]
     float last_ms = 0.0f;
     bool timing_valid = false;
     std::string err;
@@ -568,6 +575,9 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         F.tiles_y = (F.local_rows + bh - 1) / bh;
     }
     F.num_blocks = F.tiles_x * F.tiles_y;
+    F.work_counter = nullptr;
+    F.tiles8_x = (w + 7) / 8;
+    F.num_tiles8 = F.tiles8_x * ((F.local_rows + 7) / 8);
     F.tile_order = nullptr;
     F.tile_cost = nullptr;
 
@@ -604,9 +614,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         O.wave_times = c->d_wt;
     }
 #endif
+    // first_bounce_kernel with persistent waves schedules 8x8 tiles, the others blocks
+    const bool persistent = wavefront && RTK_PERSISTENT;
+    const uint32_t units = persistent ? F.num_tiles8 : F.num_blocks;
     // static block order (in-kernel XCD chunk dealing, or a host-built table)
     F.tile_order = nullptr;
-    const int pol = tile_order_policy();
+    const int pol = persistent ? 0 : tile_order_policy();
     if (pol != 0) {
         if (c->order_policy != pol || c->order_tx != F.tiles_x || c->order_ty != F.tiles_y) {
             const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y, pol);
@@ -623,12 +636,13 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.tile_cost = nullptr;
     bool lpt = false;
     if (!(flags & RT_FLAG_STATIC_ORDER)) {
-        if ((rc = ensure(c, c->d_cost, c->cost_cap, F.num_blocks))) return rc;
-        if ((rc = ensure(c, c->d_lpt, c->lpt_cap, F.num_blocks))) return rc;
+        if ((rc = ensure(c, c->d_cost, c->cost_cap, units))) return rc;
+        if ((rc = ensure(c, c->d_lpt, c->lpt_cap, units))) return rc;
         const uint64_t key = ((uint64_t)F.tiles_x << 48) ^ ((uint64_t)F.tiles_y << 32) ^ F.local_rows ^
-                             ((uint64_t)c->scene_gen << 20) ^ (wavefront ? (1ull << 63) : 0ull);
+                             ((uint64_t)c->scene_gen << 20) ^ (wavefront ? (1ull << 63) : 0ull) ^
+                             (persistent ? (1ull << 62) : 0ull);
         if (key != c->cost_key) {
-            HIPC(c, hipMemsetAsync(c->d_cost, 0, (size_t)F.num_blocks * 4, s));
+            HIPC(c, hipMemsetAsync(c->d_cost, 0, (size_t)units * 4, s));
             c->cost_key = key;
             c->cost_ready = false;
         }
@@ -640,8 +654,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const int ax = aux ? 1 : 0;
     HIPC(c, hipEventRecord(E.e[0], s));
     if (lpt) {
-        hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt,
-                           F.num_blocks);
+        hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt, units);
         F.tile_order = c->d_lpt;
     }
     if (F.tile_cost) c->cost_ready = true;
@@ -693,6 +706,20 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         // counters per bounce k: [8k+0] queue size of bounce k, [8k+1] slow size, [8k+2] fetch, [8k+3] slow fetch
         auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)c->d_wq[k & 1] : (rtk::QRay*)nullptr; };
         uint32_t* cnt = c->d_wcnt;
+        dim3 fgrid = grid;
+        if (persistent) {
+            if (!c->fb_grid[mi]) {
+                int cus = 0, b1 = 0;
+                HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+                if (hw) HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_hw::first_bounce_kernel<true>,
+                                                                             64 * RTK_FUSED_WAVES, 0));
+                else HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_strict::first_bounce_kernel<true>,
+                                                                          64 * RTK_FUSED_WAVES, 0));
+                c->fb_grid[mi] = std::max(1, b1) * cus;
+            }
+            fgrid = dim3(std::min<uint32_t>((uint32_t)c->fb_grid[mi], (F.num_tiles8 + RTK_FUSED_WAVES - 1) / RTK_FUSED_WAVES));
+            F.work_counter = cnt + 8 * (RT_MAX_DEPTH + 1) - 1;   // last counter slot, zeroed with the others
+        }
         HIPC(c, hipEventRecord(E.e[2], s));
         {
             rtk::WQ W{};
@@ -702,12 +729,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.slow_count = cnt + 8 * 0 + 1;
             W.bounce = 0;
             if (fast_kernel) {
-                if (hw) hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<true>, grid, block, 0, s, S, F, O, W, ax);
-                else hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<true>, grid, block, 0, s, S, F, O, W, ax);
+                if (hw) hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<true>, fgrid, block, 0, s, S, F, O, W, ax);
+                else hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<true>, fgrid, block, 0, s, S, F, O, W, ax);
             } else if (hw) {
-                hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<false>, grid, block, 0, s, S, F, O, W, ax);
+                hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<false>, fgrid, block, 0, s, S, F, O, W, ax);
             } else {
-                hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<false>, grid, block, 0, s, S, F, O, W, ax);
+                hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<false>, fgrid, block, 0, s, S, F, O, W, ax);
             }
         }
         HIPC(c, hipEventRecord(E.e[3], s));
