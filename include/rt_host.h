@@ -99,6 +99,18 @@ int rt_bvh_load(const rt_mesh* m, const char* path, rt_bvh** out);
 int rt_camera_params(const rt_mesh* m, uint32_t w, uint32_t h, float radius, float extra_alpha,
                      float extra_beta, const float* light_pos, const float* light_color, rt_params* out);
 
+/* Orbit camera of the interactive loop (Camera.cpp:6-68): rt_camera_create = Camera()
+ * with the given radius (reference: 200), add_rotate / add_radius as the mouse handlers
+ * call them (RayTracer.cpp:553-565, dx * 0.25 / 100 radians per pixel), and
+ * rt_camera_frame_params = updateCamera (RayTracer.cpp:609-672) for one frame. */
+typedef struct rt_camera rt_camera;
+rt_camera* rt_camera_create(float radius);
+void rt_camera_destroy(rt_camera* c);
+int rt_camera_add_rotate(rt_camera* c, float da, float db);
+int rt_camera_add_radius(rt_camera* c, float dr);
+int rt_camera_frame_params(const rt_camera* c, const rt_mesh* m, uint32_t w, uint32_t h, const float* light_pos,
+                           const float* light_color, rt_params* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,7 @@
 
 struct rt_mesh { rtamd::Mesh m; };
 struct rt_bvh { rtamd::Bvh b; };
+struct rt_camera { rtamd::Camera c; explicit rt_camera(float r) : c(r) {} };
 
 extern "C" {
 
@@ -198,6 +199,25 @@ int rt_camera_params(const rt_mesh* mh, uint32_t w, uint32_t h, float radius, fl
                      const float* light_pos, const float* light_color, rt_params* out) {
     if (!mh || !out || w == 0 || h == 0) return RT_ERR_INVALID_ARG;
     *out = rtamd::camera_params(mh->m, w, h, radius, extra_alpha, extra_beta, light_pos, light_color);
+    return RT_OK;
+}
+
+rt_camera* rt_camera_create(float radius) { return new (std::nothrow) rt_camera(radius); }
+void rt_camera_destroy(rt_camera* c) { delete c; }
+int rt_camera_add_rotate(rt_camera* c, float da, float db) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    c->c.add_rotate(da, db);
+    return RT_OK;
+}
+int rt_camera_add_radius(rt_camera* c, float dr) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    c->c.add_radius(dr);
+    return RT_OK;
+}
+int rt_camera_frame_params(const rt_camera* c, const rt_mesh* mh, uint32_t w, uint32_t h, const float* light_pos,
+                           const float* light_color, rt_params* out) {
+    if (!c || !mh || !out || w == 0 || h == 0) return RT_ERR_INVALID_ARG;
+    *out = rtamd::frame_params(c->c, mh->m, w, h, light_pos, light_color);
     return RT_OK;
 }
 

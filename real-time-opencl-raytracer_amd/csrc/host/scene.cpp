@@ -344,44 +344,55 @@ inline V3 normv(V3 v) {
 inline V3 scalev(float s, V3 a) { return V3{s * a.x, s * a.y, s * a.z}; }
 inline V3 addv(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 
-struct Camera {
-    V3 eye{0, 0, 0}, center{0, 0, 0}, up{0, 1, 0};
-    float cam_radius = 200.0f, cam_alpha = 0.0f, cam_beta = 0.0f;
-    V3 right{}, cup{}, dir{};
-    explicit Camera(float radius) : cam_radius(radius) {
-        add_rotate((float)(45 * (3 + 2) * M_PI / 180.0f), (float)(45 * M_PI / 180.0f));
-    }
-    void add_rotate(float da, float db) {
-        cam_alpha += da;
-        cam_beta += db;
-        if (cam_beta < 0.0f) cam_beta = (float)(cam_beta + 2.0f * M_PI);
-        else if (cam_beta > 2.0f * M_PI) cam_beta = (float)(cam_beta - 2.0f * M_PI);
-        if ((cam_beta > M_PI / 2.0f) && (cam_beta < 3.0f * M_PI / 2.0f)) up = V3{0.0f, -1.0f, 0.0f};
-        else up = V3{0.0f, 1.0f, 0.0f};
-        eye.x = center.x + cam_radius * std::cos(cam_beta) * std::cos(cam_alpha);
-        eye.y = center.y + cam_radius * std::sin(cam_beta);
-        eye.z = center.z + cam_radius * std::cos(cam_beta) * std::sin(cam_alpha);
-        dir = normv(V3{center.x - eye.x, center.y - eye.y, center.z - eye.z});
-        right = normv(crossv(dir, up));
-        V3 cu = crossv(dir, right);
-        cup = normv(V3{-cu.x, -cu.y, -cu.z});
-    }
-};
 }  // namespace
 
-rt_params camera_params(const Mesh& m, uint32_t w, uint32_t h, float radius, float extra_alpha,
-                        float extra_beta, const float* light_pos, const float* light_color) {
-    Camera cam(radius);
-    if (extra_alpha != 0.0f || extra_beta != 0.0f) cam.add_rotate(extra_alpha, extra_beta);
+Camera::Camera(float radius) : cam_radius(radius) {  // Camera() (Camera.cpp:6-19)
+    add_rotate((float)(45 * (3 + 2) * M_PI / 180.0f), (float)(45 * M_PI / 180.0f));
+}
+
+void Camera::add_rotate(float da, float db) {  // Camera.cpp:26-46
+    cam_alpha += da;
+    cam_beta += db;
+    if (cam_beta < 0.0f) cam_beta = (float)(cam_beta + 2.0f * M_PI);
+    else if (cam_beta > 2.0f * M_PI) cam_beta = (float)(cam_beta - 2.0f * M_PI);
+    if ((cam_beta > M_PI / 2.0f) && (cam_beta < 3.0f * M_PI / 2.0f)) up[0] = 0.0f, up[1] = -1.0f, up[2] = 0.0f;
+    else up[0] = 0.0f, up[1] = 1.0f, up[2] = 0.0f;
+    update_eye();
+}
+
+void Camera::add_radius(float dr) {  // Camera.cpp:21-24
+    cam_radius += dr;
+    update_eye();
+}
+
+void Camera::update_eye() {  // Camera.cpp:48-68 (update_eye + update_full)
+    eye[0] = center[0] + cam_radius * std::cos(cam_beta) * std::cos(cam_alpha);
+    eye[1] = center[1] + cam_radius * std::sin(cam_beta);
+    eye[2] = center[2] + cam_radius * std::cos(cam_beta) * std::sin(cam_alpha);
+    const V3 e{eye[0], eye[1], eye[2]}, u{up[0], up[1], up[2]};
+    const V3 d = normv(V3{center[0] - e.x, center[1] - e.y, center[2] - e.z});
+    const V3 r = normv(crossv(d, u));
+    const V3 cu = crossv(d, r);
+    const V3 c = normv(V3{-cu.x, -cu.y, -cu.z});
+    dir[0] = d.x; dir[1] = d.y; dir[2] = d.z;
+    right[0] = r.x; right[1] = r.y; right[2] = r.z;
+    cup[0] = c.x; cup[1] = c.y; cup[2] = c.z;
+}
+
+// updateCamera (RayTracer.cpp:609-672): Params from the camera, the frame size and the scene box
+rt_params frame_params(const Camera& cam, const Mesh& m, uint32_t w, uint32_t h, const float* light_pos,
+                       const float* light_color) {
     const float FOV = 60.0f;
     float theta = (float)((FOV * 3.1415 * 0.5) / 180.0f);
     float half_width = std::tan(theta);
     float aspect = (float)w / (float)h;
     float u0 = -half_width * aspect, v0 = -half_width, u1 = half_width * aspect, v1 = half_width;
     float dist_to_image = 1;
-    V3 a = scalev(u1 - u0, cam.right);
-    V3 b = scalev(v1 - v0, cam.cup);
-    V3 c = addv(addv(addv(cam.eye, scalev(u0, cam.right)), scalev(v0, cam.cup)), scalev(dist_to_image, cam.dir));
+    const V3 right{cam.right[0], cam.right[1], cam.right[2]}, cup{cam.cup[0], cam.cup[1], cam.cup[2]};
+    const V3 dir{cam.dir[0], cam.dir[1], cam.dir[2]}, eye{cam.eye[0], cam.eye[1], cam.eye[2]};
+    V3 a = scalev(u1 - u0, right);
+    V3 b = scalev(v1 - v0, cup);
+    V3 c = addv(addv(addv(eye, scalev(u0, right)), scalev(v0, cup)), scalev(dist_to_image, dir));
     const float lp_def[3] = {-23.0f, 200.0f, 3.0f}, lc_def[3] = {1.0f, 1.0f, 1.0f};
     const float* lp = light_pos ? light_pos : lp_def;
     const float* lc = light_color ? light_color : lc_def;
@@ -389,12 +400,19 @@ rt_params camera_params(const Mesh& m, uint32_t w, uint32_t h, float radius, flo
     p.a = f4(a.x, a.y, a.z, 1.0f);
     p.b = f4(b.x, b.y, b.z, 1.0f);
     p.c = f4(c.x, c.y, c.z, 1.0f);
-    p.campos = f4(cam.eye.x, cam.eye.y, cam.eye.z, 1.0f);
+    p.campos = f4(eye.x, eye.y, eye.z, 1.0f);
     p.light_pos = f4(lp[0], lp[1], lp[2], 1.0f);
     p.light_color = f4(lc[0], lc[1], lc[2], 1.0f);
     p.scene_aabb_min = f4(m.scene_min[0], m.scene_min[1], m.scene_min[2], 1.0f);
     p.scene_aabb_max = f4(m.scene_max[0], m.scene_max[1], m.scene_max[2], 1.0f);
     return p;
+}
+
+rt_params camera_params(const Mesh& m, uint32_t w, uint32_t h, float radius, float extra_alpha,
+                        float extra_beta, const float* light_pos, const float* light_color) {
+    Camera cam(radius);
+    if (extra_alpha != 0.0f || extra_beta != 0.0f) cam.add_rotate(extra_alpha, extra_beta);
+    return frame_params(cam, m, w, h, light_pos, light_color);
 }
 
 }  // namespace rtamd

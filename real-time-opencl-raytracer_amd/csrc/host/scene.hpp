@@ -55,6 +55,19 @@ void build_bvh(const Mesh& m, int max_leaf, int num_threads, Bvh& out);
 // The reference SplitBVHBuilder (SplitBVHBuilder.cpp:41-476) + BVH_Cuda::build_from_bvh2, same bytes.
 void build_sbvh(const Mesh& m, int num_threads, Bvh& out);
 
+// Camera (Camera.cpp:6-68): orbit around the origin; angles accumulate in float as the reference's do.
+struct Camera {
+    float eye[3] = {0, 0, 0}, center[3] = {0, 0, 0}, up[3] = {0, 1, 0};
+    float cam_radius = 200.0f, cam_alpha = 0.0f, cam_beta = 0.0f;
+    float right[3] = {0, 0, 0}, cup[3] = {0, 0, 0}, dir[3] = {0, 0, 0};
+    explicit Camera(float radius);
+    void add_rotate(float da, float db);
+    void add_radius(float dr);
+    void update_eye();
+};
+rt_params frame_params(const Camera& cam, const Mesh& m, uint32_t w, uint32_t h, const float* light_pos,
+                       const float* light_color);
+
 rt_params camera_params(const Mesh& m, uint32_t w, uint32_t h, float radius, float extra_alpha,
                         float extra_beta, const float* light_pos, const float* light_color);
 

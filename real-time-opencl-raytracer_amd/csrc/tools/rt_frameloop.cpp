@@ -1,0 +1,165 @@
+// rt_frameloop -- headless stand-in for the reference's interactive GLUT loop
+// (SURVEY.md 8f #4): displayGL = updateCamera + render (RayTracer.cpp:284-293),
+// the FPS title once a second (:497-516), and the right-button orbit drag
+// (motion, :553-565: add_rotate(dx * 0.25 / 100, dy * 0.25 / 100)), driven by a
+// fixed per-frame drag instead of a mouse.  Frames go through the C ABI exactly
+// as the reference's host path does: rt_set_params (clEnqueueWriteBuffer of
+// Params, :671) then rt_render (launch + finish + blocking read-back, :330-344).
+// Optional PPM dumps replace the window.
+//
+//   rt_frameloop [--dae F | --obj F | --scene cornell|knot|heightfield] [--bvh-cache F]
+//                [--width W] [--height H] [--depth D] [--frames N] [--drag DX DY]
+//                [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F]
+//
+// Prints "N.N fps" lines and a final JSON summary.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_abi.h"
+#include "rt_host.h"
+
+namespace {
+
+struct Args {
+    std::string dae, obj, scene = "heightfield", bvh_cache, ppm_dir;
+    uint32_t w = 1024, h = 768;  // RayTracer.cpp:39-40 (WIDTH, HEIGHT)
+    int depth = 3, frames = 120, ppm_every = 0, device = 0;
+    uint32_t flags = 0;
+    float dx = 4.0f, dy = 0.0f;
+};
+
+int usage() {
+    std::fprintf(stderr,
+                 "usage: rt_frameloop [--dae F | --obj F | --scene cornell|knot|heightfield] [--bvh-cache F]\n"
+                 "                    [--width W] [--height H] [--depth D] [--frames N] [--drag DX DY]\n"
+                 "                    [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F]\n");
+    return 2;
+}
+
+bool parse(int argc, char** argv, Args& a) {
+    for (int i = 1; i < argc; ++i) {
+        const std::string k = argv[i];
+        auto need = [&](int n) { return i + n < argc; };
+        if (k == "--dae" && need(1)) a.dae = argv[++i];
+        else if (k == "--obj" && need(1)) a.obj = argv[++i];
+        else if (k == "--scene" && need(1)) a.scene = argv[++i];
+        else if (k == "--bvh-cache" && need(1)) a.bvh_cache = argv[++i];
+        else if (k == "--width" && need(1)) a.w = (uint32_t)std::atoi(argv[++i]);
+        else if (k == "--height" && need(1)) a.h = (uint32_t)std::atoi(argv[++i]);
+        else if (k == "--depth" && need(1)) a.depth = std::atoi(argv[++i]);
+        else if (k == "--frames" && need(1)) a.frames = std::atoi(argv[++i]);
+        else if (k == "--drag" && need(2)) { a.dx = (float)std::atof(argv[++i]); a.dy = (float)std::atof(argv[++i]); }
+        else if (k == "--ppm-dir" && need(1)) a.ppm_dir = argv[++i];
+        else if (k == "--ppm-every" && need(1)) a.ppm_every = std::atoi(argv[++i]);
+        else if (k == "--device" && need(1)) a.device = std::atoi(argv[++i]);
+        else if (k == "--flags" && need(1)) a.flags = (uint32_t)std::strtoul(argv[++i], nullptr, 0);
+        else return false;
+    }
+    return a.w > 0 && a.h > 0 && a.frames > 0 && a.depth >= 0 && a.depth <= RT_MAX_DEPTH;
+}
+
+// Packed pixels are b<<16 | g<<8 | r (volumeRender.cl:186-195); row 0 is the first image row.
+bool write_ppm(const std::string& path, const std::vector<uint32_t>& px, uint32_t w, uint32_t h) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    std::fprintf(f, "P6\n%u %u\n255\n", w, h);
+    std::vector<unsigned char> row((size_t)w * 3);
+    for (uint32_t y = 0; y < h; ++y) {
+        for (uint32_t x = 0; x < w; ++x) {
+            const uint32_t p = px[(size_t)y * w + x];
+            row[3 * x + 0] = (unsigned char)(p & 0xFF);
+            row[3 * x + 1] = (unsigned char)((p >> 8) & 0xFF);
+            row[3 * x + 2] = (unsigned char)((p >> 16) & 0xFF);
+        }
+        std::fwrite(row.data(), 1, row.size(), f);
+    }
+    return std::fclose(f) == 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Args a;
+    if (!parse(argc, argv, a)) return usage();
+    using clk = std::chrono::steady_clock;
+
+    rt_mesh* mesh = rt_mesh_create();
+    int rc;
+    if (!a.dae.empty()) rc = rt_mesh_load_dae(mesh, a.dae.c_str());
+    else if (!a.obj.empty()) rc = rt_mesh_load_obj(mesh, a.obj.c_str());
+    else if (a.scene == "cornell") rc = rt_mesh_gen_cornell(mesh);
+    else if (a.scene == "knot") rc = rt_mesh_gen_torus_knot(mesh, 256, 137);
+    else if (a.scene == "heightfield") rc = rt_mesh_gen_heightfield(mesh, 500, 1000, 10.0f, 0x5EED, -150, 650, -150, 650);
+    else return usage();
+    if (rc != RT_OK) { std::fprintf(stderr, "scene load failed (%d)\n", rc); return 1; }
+
+    // BVH: the cache when it matches the mesh, else the reference's spatial-split build
+    const auto tb = clk::now();
+    rt_bvh* bvh = nullptr;
+    bool cached = false;
+    if (!a.bvh_cache.empty() && rt_bvh_load(mesh, a.bvh_cache.c_str(), &bvh) == RT_OK) cached = true;
+    if (!bvh) {
+        if ((rc = rt_bvh_build_sbvh(mesh, 0, &bvh)) != RT_OK) { std::fprintf(stderr, "bvh build failed\n"); return 1; }
+        if (!a.bvh_cache.empty()) rt_bvh_save(bvh, mesh, a.bvh_cache.c_str());
+    }
+    const double bvh_s = std::chrono::duration<double>(clk::now() - tb).count();
+
+    rt_mesh_view mv;
+    rt_bvh_view bv;
+    rt_mesh_view_get(mesh, &mv);
+    rt_bvh_view_get(bvh, &bv);
+    rt_ctx* ctx = nullptr;
+    if ((rc = rt_create(a.device, &ctx)) != RT_OK) { std::fprintf(stderr, "rt_create: %s\n", rt_last_error(nullptr)); return 1; }
+    rc = rt_upload_scene(ctx, mv.vertices, mv.num_vertices, mv.indices, mv.num_indices, bv.nodes, bv.num_nodes,
+                         bv.tri_indices, bv.num_tri_indices, mv.normals, mv.num_normals, mv.normals_indices,
+                         mv.materials, mv.num_materials, mv.tri_to_material);
+    if (rc != RT_OK) { std::fprintf(stderr, "rt_upload_scene: %s\n", rt_last_error(ctx)); return 1; }
+
+    rt_camera* cam = rt_camera_create(200.0f);
+    std::vector<uint32_t> px((size_t)a.w * a.h);
+    int frames_in_second = 0, total = 0;
+    double kernel_ms_sum = 0.0;
+    auto t0 = clk::now(), tsec = t0;
+    for (int f = 0; f < a.frames; ++f) {
+        if (f > 0) rt_camera_add_rotate(cam, a.dx * 0.25f / 100.0f, a.dy * 0.25f / 100.0f);  // motion()
+        rt_params p;
+        rt_camera_frame_params(cam, mesh, a.w, a.h, nullptr, nullptr, &p);   // updateCamera()
+        if ((rc = rt_set_params(ctx, &p)) != RT_OK ||
+            (rc = rt_render(ctx, a.w, a.h, a.depth, a.flags, px.data(), nullptr)) != RT_OK) {
+            std::fprintf(stderr, "frame %d: %s\n", f, rt_last_error(ctx));
+            return 1;
+        }
+        float kt = 0.0f, kk = 0.0f;
+        if (rt_last_timing(ctx, &kt, &kk) == RT_OK) kernel_ms_sum += kt;
+        ++frames_in_second;
+        ++total;
+        if (a.ppm_every > 0 && !a.ppm_dir.empty() && f % a.ppm_every == 0) {
+            char name[64];
+            std::snprintf(name, sizeof name, "/frame_%05d.ppm", f);
+            if (!write_ppm(a.ppm_dir + name, px, a.w, a.h)) std::fprintf(stderr, "cannot write %s\n", name);
+        }
+        const auto now = clk::now();
+        const double since = std::chrono::duration<double>(now - tsec).count();
+        if (since >= 1.0) {  // update(): the window title's fps, once a second
+            std::printf("%.1f fps\n", frames_in_second / since);
+            std::fflush(stdout);
+            frames_in_second = 0;
+            tsec = now;
+        }
+    }
+    const double wall = std::chrono::duration<double>(clk::now() - t0).count();
+    std::printf("{\"frames\": %d, \"width\": %u, \"height\": %u, \"depth\": %d, \"fps\": %.2f, \"ms_per_frame\": %.4f, "
+                "\"kernel_ms_per_frame\": %.4f, \"triangles\": %d, \"bvh_nodes\": %d, \"bvh_cached\": %s, "
+                "\"bvh_seconds\": %.3f}\n",
+                total, a.w, a.h, a.depth, total / wall, 1e3 * wall / total, kernel_ms_sum / total,
+                mv.num_indices / 3, bv.num_nodes, cached ? "true" : "false", bvh_s);
+    rt_camera_destroy(cam);
+    rt_destroy(ctx);
+    rt_bvh_destroy(bvh);
+    rt_mesh_destroy(mesh);
+    return 0;
+}

@@ -86,7 +86,8 @@ HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mes
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
                 "rt_mesh_gen_cornell", "rt_mesh_gen_torus_knot", "rt_mesh_gen_heightfield", "rt_mesh_gen_random",
                 "rt_mesh_append_grid", "rt_bvh_build", "rt_bvh_build_sbvh", "rt_bvh_view_get", "rt_bvh_destroy", "rt_bvh_save",
-                "rt_bvh_load", "rt_camera_params"]
+                "rt_bvh_load", "rt_camera_params", "rt_camera_create", "rt_camera_destroy", "rt_camera_add_rotate",
+                "rt_camera_add_radius", "rt_camera_frame_params"]
 
 _lib = None
 
@@ -139,6 +140,11 @@ def lib() -> C.CDLL:
             "rt_bvh_save": (C.c_int, [vp, vp, C.c_char_p]),
             "rt_bvh_load": (C.c_int, [vp, C.c_char_p, C.POINTER(vp)]),
             "rt_camera_params": (C.c_int, [vp, u32, u32, f32, f32, f32, vp, vp, C.POINTER(rt_params)]),
+            "rt_camera_create": (vp, [f32]),
+            "rt_camera_destroy": (None, [vp]),
+            "rt_camera_add_rotate": (C.c_int, [vp, f32, f32]),
+            "rt_camera_add_radius": (C.c_int, [vp, f32]),
+            "rt_camera_frame_params": (C.c_int, [vp, vp, u32, u32, vp, vp, C.POINTER(rt_params)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -325,6 +331,31 @@ class Mesh:
         _check(lib().rt_camera_params(self._h, w, h, radius, extra_alpha, extra_beta, _ptr(lp), _ptr(lc),
                                       C.byref(p)))
         return p
+
+
+class Camera:
+    """The reference's orbit camera (Camera.cpp:6-68) + updateCamera (RayTracer.cpp:609-672)."""
+
+    def __init__(self, radius: float = 200.0):
+        self._h = lib().rt_camera_create(radius)
+        if not self._h:
+            raise MemoryError("rt_camera_create")
+
+    def add_rotate(self, da: float, db: float) -> None:
+        _check(lib().rt_camera_add_rotate(self._h, da, db))
+
+    def add_radius(self, dr: float) -> None:
+        _check(lib().rt_camera_add_radius(self._h, dr))
+
+    def params(self, mesh: "Mesh", w: int, h: int) -> rt_params:
+        p = rt_params()
+        _check(lib().rt_camera_frame_params(self._h, mesh._h, w, h, None, None, C.byref(p)))
+        return p
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().rt_camera_destroy(self._h)
+            self._h = None
 
 
 class Bvh:
