@@ -63,6 +63,9 @@
 #ifndef RTK_WAVE_TIMES
 #define RTK_WAVE_TIMES 0    // diagnostic build: per-pixel start/end timestamps (env RTAMD_WAVE_TIMES=file)
 #endif
+#ifndef RTK_PROBE_VALU
+#define RTK_PROBE_VALU 0
+#endif
 #ifndef RTK_PROBE_EXTRA_LOAD
 #define RTK_PROBE_EXTRA_LOAD 0
 #endif
