@@ -54,6 +54,9 @@
 #ifndef RTK_MIN_WAVES
 #define RTK_MIN_WAVES 7     // __launch_bounds__ minimum waves per SIMD (fused kernel)
 #endif
+#ifndef RTK_MULTI_MIN_WAVES
+#define RTK_MULTI_MIN_WAVES 7   // render_kernel / wf_bounce_kernel (multi-bounce state)
+#endif
 #ifndef RTK_TILE_ORDER
 #define RTK_TILE_ORDER 1   // fused-kernel tile order policy (tile_order_table), env RTAMD_TILE_ORDER
 #endif
