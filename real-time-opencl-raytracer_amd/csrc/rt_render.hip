@@ -655,7 +655,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         lpt = c->cost_ready;
         F.tile_cost = c->d_cost;
     }
-    const bool fast_kernel = S.fast_div != 0 && S.clean != 0;
+    const bool fast_kernel = S.clean != 0;   // any quotient domain: traverse_fast picks the variant
     const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
     const int ax = aux ? 1 : 0;
     HIPC(c, hipEventRecord(E.e[0], s));
