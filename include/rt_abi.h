@@ -151,19 +151,20 @@ int rt_render_device(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_
 int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* tiling);
 
 /* Kernel-side timing of the last render, from HIP events on the launch stream
- * (ms): total_ms = every kernel of the frame (block-order build, the fused
- * render kernel, the deferred-pixel kernel); traverse_ms = the fused render
- * kernel alone (what the roofline is computed on; total_ms for the pipelined
- * RT_FLAG_WAVEFRONT path). */
+ * (ms): total_ms = every kernel of the frame (counter reset / block-order
+ * build, the first-bounce or fused render kernel, further bounces);
+ * traverse_ms = the frame's main kernel alone (first_bounce_kernel for depth 1
+ * and the wavefront path, else the fused render kernel: what the roofline is
+ * computed on). */
 int rt_last_timing(rt_ctx* ctx, float* total_ms, float* traverse_ms);
 /* The same two times averaged over the last n frames (n <= 64 and <= frames
  * rendered): bench.py reads the timed steps' kernel time this way, without a
  * host sync inside its timed loop. */
 int rt_timing_average(rt_ctx* ctx, int32_t n, float* total_ms, float* traverse_ms);
 
-/* Pixels of the last fused-kernel frame that the fast kernel handed back to the
- * general kernel (a ray outside the 3-op quotient's domain, or a stack deeper
- * than the LDS part); diagnostics, synchronizes the device. */
+/* Traversals of the last frame that outgrew the fast kernel's LDS stack and
+ * restarted in-kernel with the general traversal (same result, slower ray);
+ * diagnostics, synchronizes the stream. */
 int rt_last_deferred(rt_ctx* ctx, uint32_t* count);
 
 /* Device stack-overflow counter (reference: silent miss, volumeRender.cl:914). */

@@ -126,8 +126,6 @@ struct WQ {
     const uint32_t* perm;     // optional order of `in` (sorted), or null
     QRay* out;                // next bounce's rays
     uint32_t* out_count;
-    QRay* slow;               // rays of this bounce the fast code hands back
-    uint32_t* slow_count;
     uint32_t* fetch;          // dynamic work counter of this launch
     int bounce;
 };
@@ -139,8 +137,7 @@ struct Outputs {
     float* rgb;
     uint32_t* gstack;            // [kGlobalStack][local_pixels]
     unsigned long long* overflow;
-    uint32_t* defer;             // pixels handed back by the fast kernel (render_list_kernel)
-    uint32_t* defer_count;
+    uint32_t* restarts;          // traversals that outgrew the LDS stack and restarted (general code)
     uint64_t local_pixels;
     uint32_t* wave_times;        // RTK_WAVE_TIMES diagnostic: per pixel {start, end, hw_id, xcc_id}
 };
@@ -218,13 +215,11 @@ struct rt_ctx {
     unsigned long long* d_overflow = nullptr;
     // pipelined path buffers (per local pixel) + persistent grid sizes
     float4* d_wq[2] = {nullptr, nullptr}; size_t wq_cap[2] = {0, 0};   // wavefront ray queues (ping-pong)
-    float4* d_wslow = nullptr; size_t wslow_cap = 0;                    // rays handed to the general code
-    uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // per-bounce counters
+    uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // frame counters (kCounters)
     uint32_t* d_sort[4] = {nullptr, nullptr, nullptr, nullptr}; size_t sort_cap[4] = {0, 0, 0, 0};
     uint8_t* d_sort_tmp = nullptr; size_t sort_tmp_cap = 0;
     uint32_t* d_rank = nullptr;                                         // triangle -> first leaf position
     uint32_t* d_wt = nullptr; size_t wt_cap = 0;             // RTK_WAVE_TIMES
-    uint32_t* d_defer = nullptr; size_t defer_cap = 0;       // [4 + P]: count, then deferred pixels
     uint32_t* d_order = nullptr; size_t order_cap = 0;        // tile order table for the fused kernel
     uint32_t order_tx = 0, order_ty = 0; int order_policy = -1;
     uint32_t* d_cost = nullptr; size_t cost_cap = 0;          // adaptive order: last frame's per-tile times
@@ -239,6 +234,10 @@ struct rt_ctx {
 };
 
 static std::string g_err;
+
+// frame counter buffer (d_wcnt): 8 per bounce, then the restart count
+constexpr size_t kRestartSlot = 8 * (RT_MAX_DEPTH + 1);
+constexpr size_t kCounters = kRestartSlot + 1;
 
 static int set_err(rt_ctx* c, const std::string& m, int code) {
     if (c) c->err = m; else g_err = m;
@@ -362,9 +361,9 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_gstack) (void)hipFree(c->d_gstack);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
-    for (void* p : {(void*)c->d_wq[0], (void*)c->d_wq[1], (void*)c->d_wslow, (void*)c->d_wcnt, (void*)c->d_sort[0],
+    for (void* p : {(void*)c->d_wq[0], (void*)c->d_wq[1], (void*)c->d_wcnt, (void*)c->d_sort[0],
                     (void*)c->d_sort[1], (void*)c->d_sort[2], (void*)c->d_sort[3], (void*)c->d_sort_tmp,
-                    (void*)c->d_defer, (void*)c->d_order, (void*)c->d_wt,
+                    (void*)c->d_order, (void*)c->d_wt,
                     (void*)c->d_cost, (void*)c->d_lpt})
         if (p) (void)hipFree(p);
     for (auto& f : c->ring)
@@ -610,9 +609,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
 
     if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
     O.gstack = c->d_gstack;
-    if ((rc = ensure(c, c->d_defer, c->defer_cap, (size_t)npix + 4))) return rc;
-    O.defer = c->d_defer + 4;
-    O.defer_count = c->d_defer;
+    // frame counters: [8k + 0] queue size of bounce k, [8k + 2] its fetch cursor,
+    // [kRestartSlot] restarted traversals; zeroed by the frame's first launch
+    if ((rc = ensure(c, c->d_wcnt, c->wcnt_cap, kCounters))) return rc;
+    O.restarts = c->d_wcnt + kRestartSlot;
 #if RTK_WAVE_TIMES
     if (std::getenv("RTAMD_WAVE_TIMES")) {
         if ((rc = ensure(c, c->d_wt, c->wt_cap, (size_t)npix * 4))) return rc;
@@ -656,17 +656,18 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         F.tile_cost = c->d_cost;
     }
     const bool fast_kernel = S.clean != 0;   // any quotient domain: traverse_fast picks the variant
-    const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES), lgrid(64), lblock(256);
+    const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES);
     const int ax = aux ? 1 : 0;
     HIPC(c, hipEventRecord(E.e[0], s));
-    if (lpt) {
-        hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt, units);
-        F.tile_order = c->d_lpt;
-    }
+    // first launch: zero the counters (all of them for the wavefront queues, else the
+    // restart count) and, with a measured previous frame, build the longest-first order
+    hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt,
+                       lpt ? units : 0u, wavefront ? c->d_wcnt : c->d_wcnt + kRestartSlot,
+                       wavefront ? (uint32_t)kCounters : 1u);
+    if (lpt) F.tile_order = c->d_lpt;
     if (F.tile_cost) c->cost_ready = true;
 
     if (!wavefront) {
-        if (fast_kernel) HIPC(c, hipMemsetAsync(c->d_defer, 0, 16, s));
         HIPC(c, hipEventRecord(E.e[2], s));
         if (fast_kernel) {
             if (hw) hipLaunchKernelGGL(rtk_hw::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
@@ -678,15 +679,11 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         }
         HIPC(c, hipEventRecord(E.e[3], s));
         E.has_k = true;
-        if (fast_kernel) {  // the (normally empty) list of pixels the fast kernel handed back
-            if (hw) hipLaunchKernelGGL(rtk_hw::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
-            else hipLaunchKernelGGL(rtk_strict::render_list_kernel, lgrid, lblock, 0, s, S, F, O, ax);
-        }
         HIPC(c, hipGetLastError());
         HIPC(c, hipEventRecord(E.e[1], s));
     } else {
         // Wavefront: bounce 0 over tiles, then one persistent launch per further bounce
-        // over the queue of rays still in flight (+ the general code for handed-back rays).
+        // over the queue of rays still in flight.
         const int mi = hw ? 1 : 0;
         if (!c->wf_grid[mi]) {
             int cus = 0, b1 = 0;
@@ -698,8 +695,6 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         const size_t qcap = (size_t)npix * 3;  // float4 per QRay x 3
         if (depth > 1 && (rc = ensure(c, c->d_wq[0], c->wq_cap[0], qcap))) return rc;
         if (depth > 1 && (rc = ensure(c, c->d_wq[1], c->wq_cap[1], qcap))) return rc;
-        if ((rc = ensure(c, c->d_wslow, c->wslow_cap, qcap))) return rc;
-        if ((rc = ensure(c, c->d_wcnt, c->wcnt_cap, 8 * (RT_MAX_DEPTH + 1)))) return rc;
         const bool sort = (flags & RT_FLAG_WF_SORT) && depth > 1 && c->d_rank;
         if (sort) {
             for (int i = 0; i < 4; ++i)
@@ -708,8 +703,6 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             HIPC(c, rtk_sort_temp_bytes((int)npix, need));
             if ((rc = ensure(c, c->d_sort_tmp, c->sort_tmp_cap, need))) return rc;
         }
-        HIPC(c, hipMemsetAsync(c->d_wcnt, 0, 8 * (RT_MAX_DEPTH + 1) * sizeof(uint32_t), s));
-        // counters per bounce k: [8k+0] queue size of bounce k, [8k+1] slow size, [8k+2] fetch, [8k+3] slow fetch
         auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)c->d_wq[k & 1] : (rtk::QRay*)nullptr; };
         uint32_t* cnt = c->d_wcnt;
         dim3 fgrid = grid;
@@ -724,15 +717,13 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
                 c->fb_grid[mi] = std::max(1, b1) * cus;
             }
             fgrid = dim3(std::min<uint32_t>((uint32_t)c->fb_grid[mi], (F.num_tiles8 + RTK_FUSED_WAVES - 1) / RTK_FUSED_WAVES));
-            F.work_counter = cnt + 8 * (RT_MAX_DEPTH + 1) - 1;   // last counter slot, zeroed with the others
+            F.work_counter = cnt + kRestartSlot - 1;   // last per-bounce slot, zeroed with the others
         }
         HIPC(c, hipEventRecord(E.e[2], s));
         {
             rtk::WQ W{};
             W.out = qbuf(1);
             W.out_count = cnt + 8 * 1 + 0;
-            W.slow = (rtk::QRay*)c->d_wslow;
-            W.slow_count = cnt + 8 * 0 + 1;
             W.bounce = 0;
             if (fast_kernel) {
                 if (hw) hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<true>, fgrid, block, 0, s, S, F, O, W, ax);
@@ -745,49 +736,31 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         }
         HIPC(c, hipEventRecord(E.e[3], s));
         E.has_k = true;
-        for (int k = 0; k < depth; ++k) {
-            if (k > 0) {  // fast launch of bounce k over its queue
-                rtk::WQ W{};
-                W.in = qbuf(k);
-                W.in_count = cnt + 8 * k + 0;
-                W.perm = nullptr;
-                if (sort) {
-                    hipLaunchKernelGGL(rtk_strict::wf_key_kernel, dim3(1024), dim3(256), 0, s,
-                                       (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, c->d_sort[0],
-                                       c->d_sort[1], c->d_rank);
-                    HIPC(c, rtk_sort_pairs(c->d_sort_tmp, c->sort_tmp_cap, c->d_sort[0], c->d_sort[2], c->d_sort[1],
-                                           c->d_sort[3], (int)npix, s));
-                    W.perm = c->d_sort[3];
-                }
-                W.out = qbuf(k + 1);
-                W.out_count = cnt + 8 * (k + 1) + 0;
-                W.slow = (rtk::QRay*)c->d_wslow;
-                W.slow_count = cnt + 8 * k + 1;
-                W.fetch = cnt + 8 * k + 2;
-                W.bounce = k;
-                const dim3 pg(c->wf_grid[mi]);
-                if (fast_kernel) {
-                    if (hw) hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
-                    else hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
-                } else if (hw) {
-                    hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
-                } else {
-                    hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
-                }
+        for (int k = 1; k < depth; ++k) {  // bounce k over its queue
+            rtk::WQ W{};
+            W.in = qbuf(k);
+            W.in_count = cnt + 8 * k + 0;
+            W.perm = nullptr;
+            if (sort) {
+                hipLaunchKernelGGL(rtk_strict::wf_key_kernel, dim3(1024), dim3(256), 0, s,
+                                   (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, c->d_sort[0],
+                                   c->d_sort[1], c->d_rank);
+                HIPC(c, rtk_sort_pairs(c->d_sort_tmp, c->sort_tmp_cap, c->d_sort[0], c->d_sort[2], c->d_sort[1],
+                                       c->d_sort[3], (int)npix, s));
+                W.perm = c->d_sort[3];
             }
-            if (fast_kernel) {  // general code over the rays of bounce k the fast code handed back
-                rtk::WQ W{};
-                W.in = (rtk::QRay*)c->d_wslow;
-                W.in_count = cnt + 8 * k + 1;
-                W.perm = nullptr;
-                W.out = qbuf(k + 1);
-                W.out_count = cnt + 8 * (k + 1) + 0;
-                W.slow = nullptr;
-                W.slow_count = nullptr;
-                W.fetch = cnt + 8 * k + 3;
-                W.bounce = k;
-                if (hw) hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<false>, lgrid, dim3(256), 0, s, S, F, O, W, ax);
-                else hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<false>, lgrid, dim3(256), 0, s, S, F, O, W, ax);
+            W.out = qbuf(k + 1);
+            W.out_count = cnt + 8 * (k + 1) + 0;
+            W.fetch = cnt + 8 * k + 2;
+            W.bounce = k;
+            const dim3 pg(c->wf_grid[mi]);
+            if (fast_kernel) {
+                if (hw) hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
+                else hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
+            } else if (hw) {
+                hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
+            } else {
+                hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
             }
         }
         HIPC(c, hipGetLastError());
@@ -877,10 +850,9 @@ int rt_timing_average(rt_ctx* c, int32_t n, float* total_ms, float* traverse_ms)
 int rt_last_deferred(rt_ctx* c, uint32_t* count) {
     if (!c || !count) return RT_ERR_INVALID_ARG;
     *count = 0;
-    if (!c->d_defer) return RT_OK;
+    if (!c->d_wcnt) return RT_OK;
     HIPC(c, hipStreamSynchronize(c->stream));
-    HIPC(c, hipDeviceSynchronize());
-    HIPC(c, hipMemcpy(count, c->d_defer, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPC(c, hipMemcpy(count, c->d_wcnt + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

@@ -448,7 +448,7 @@ class Renderer:
         return t.value, k.value
 
     def last_deferred(self) -> int:
-        """Pixels the fast kernel handed back to the general kernel in the last frame."""
+        """Traversals of the last frame that restarted with the general code (stack deeper than LDS)."""
         v = C.c_uint32()
         _check(lib().rt_last_deferred(self._h, C.byref(v)), self._h)
         return v.value

@@ -21,7 +21,7 @@ def main():
         for flags in (cfg["flags"], cfg["flags"] | rtamd.RT_FLAG_STATIC_ORDER):
             r.render_device(w, h, cfg["depth"], flags, out.data_ptr())
             torch.cuda.synchronize()
-            print(name, "flags", flags, "deferred pixels:", r.last_deferred(), "timing", r.last_timing())
+            print(name, "flags", flags, "restarted traversals:", r.last_deferred(), "timing", r.last_timing())
         r.close()
 
 
