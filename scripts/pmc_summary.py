@@ -1,4 +1,7 @@
-"""Summarise rocprofv3 --pmc CSVs for the render kernel (median over timed dispatches)."""
+"""Summarise rocprofv3 --pmc CSVs for one kernel (median over timed dispatches).
+
+Usage: pmc_summary.py [--kernel NAME] DIR...  (default: the C3 bench kernel, first_bounce_kernel)
+"""
 import csv
 import glob
 import statistics
@@ -6,7 +9,7 @@ import sys
 from collections import defaultdict
 
 
-def load(d, kernel="render_kernel"):
+def load(d, kernel="first_bounce_kernel"):
     vals = defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -16,9 +19,13 @@ def load(d, kernel="render_kernel"):
 
 
 if __name__ == "__main__":
+    args = sys.argv[1:]
+    kernel = "first_bounce_kernel"
+    if args[:1] == ["--kernel"]:
+        kernel, args = args[1], args[2:]
     m = {}
-    for d in sys.argv[1:]:
-        m.update(load(d))
+    for d in args:
+        m.update(load(d, kernel))
     for k in sorted(m):
         print(f"{k:28s} {m[k]:16.1f}")
     g = m.get
