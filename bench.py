@@ -79,7 +79,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--band-rows", type=int, default=8,
+                    help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
+    ap.add_argument("--dist", action="store_true", help="use the process-group gather path even at N = 1")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight (one stream each): frame i+1 renders while frame i drains / gathers")
+    ap.add_argument("--shard", default="", help="R/N: render only rank R's bands of an N-way split (diagnostic)")
     ap.add_argument("--direct", action="store_true", help="skip the Collada write/read of the scene")
     ap.add_argument("--bvh", default="sbvh", choices=["sbvh", "binned"],
                     help="sbvh: the reference's SplitBVHBuilder (same bytes); binned: binned-SAH object splits")
@@ -96,8 +101,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:   # rehearsal with more ranks than devices (not a bench setting)
+        local %= ndev
+    # --dist: the distributed frame path (process group, gather, assembly) even at N = 1,
+    # to exercise it on a one-GPU box
+    use_dist = world > 1 or args.dist
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -114,24 +128,40 @@ def main():
     r.upload(scene)
     r.set_params(params)
 
-    tiling = rtamd.rt_tiling(rank, world, args.band_rows, 0)
-    npx = rtamd.tiling_pixels(w, h, rank, world, args.band_rows)
-    nbands = (h + args.band_rows - 1) // args.band_rows
-    max_rows = ((nbands + world - 1) // world) * args.band_rows
-    cap = max_rows * w  # equal-size gather slots
-    out = torch.zeros(cap, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    gather = [torch.zeros(cap, dtype=torch.int32, device=dev) for _ in range(world)] if (world > 1 and rank == 0) \
-        else None
-    # at N = 1 the rank's buffer is the frame; at N > 1 rank 0 re-interleaves the gathered bands
-    frame = torch.zeros(h * w, dtype=torch.int32, device=dev) if (rank == 0 and world > 1) else None
+    # --shard R/N (diagnostic, world 1 only): render just shard R of an N-way band split,
+    # i.e. one rank's kernel work at N GPUs without the gather
+    shard_r, shard_n = rank, world
+    if args.shard:
+        if world != 1:
+            raise SystemExit("--shard is a single-process diagnostic")
+        shard_r, shard_n = (int(v) for v in args.shard.split("/"))
+    tiling = rtamd.rt_tiling(shard_r, shard_n, args.band_rows, 0)
+    npx = rtamd.tiling_pixels(w, h, shard_r, shard_n, args.band_rows)
+    cap = rtamd.tiling_pixels(w, h, 0, shard_n, args.band_rows)  # rank 0 owns the most bands
+    cap = (cap + 3) // 4 * 4                                     # 16-B aligned gather slots
+    # Frames in flight: frame i runs on stream i % F (each stream has its own frame scratch in
+    # the library, rt_render_device), so frame i+1's render overlaps frame i's tail and, at N > 1,
+    # frame i's RCCL gather.  Every launch of a frame -- render, the gather's ordering (RCCL waits
+    # on torch's current stream) and rank 0's assembly -- is on that frame's stream.  (torch's
+    # default stream is handle 0, which the C ABI would read as "the ctx's own stream".)
+    F = max(1, args.inflight)
+    streams = [torch.cuda.Stream(dev) for _ in range(F)]
+    torch.cuda.set_stream(streams[0])
+    outs = [torch.zeros(cap, dtype=torch.int32, device=dev) for _ in range(F)]
+    # rank 0: per in-flight frame one contiguous (world, cap) gather target, re-interleaved into
+    # that frame's framebuffer by one rt_assemble_bands launch
+    gbufs = [torch.zeros(world, cap, dtype=torch.int32, device=dev) for _ in range(F)] \
+        if (use_dist and rank == 0) else None
+    glists = [list(g.unbind(0)) for g in gbufs] if gbufs is not None else [None] * F
+    frames = [torch.zeros(h * w, dtype=torch.int32, device=dev) for _ in range(F)] \
+        if (rank == 0 and use_dist) else None
 
     # rays traced per frame by this rank (counted once with the aux planes)
     d = max(depth, 1)
     hits = torch.zeros(npx * d * 2, dtype=torch.int32, device=dev)
     tt = torch.zeros(npx * d, dtype=torch.float32, device=dev)
     rgb = torch.zeros(npx * 3, dtype=torch.float32, device=dev)
-    r.render_device(w, h, depth, flags, out.data_ptr(), tiling=tiling, stream=stream.cuda_stream,
+    r.render_device(w, h, depth, flags, outs[0].data_ptr(), tiling=tiling, stream=streams[0].cuda_stream,
                     aux_ptrs=(hits.data_ptr(), tt.data_ptr(), rgb.data_ptr()))
     torch.cuda.synchronize(dev)
     hv = hits.view(npx, d, 2)
@@ -139,38 +169,68 @@ def main():
     prim_local = int((hv[:, 0, 0] != -2).sum().item())
     del hits, tt, rgb
 
-    # band -> frame re-interleave (rank 0): gathered slot r holds rank r's bands in order
-    def assemble():
-        if world > 1:
-            rtamd.assemble_bands(frame, gather, w, h, args.band_rows)
+    # One step = one frame: render this rank's bands -> (N > 1) async RCCL gather of the bands
+    # to rank 0 -> rank 0 re-interleaves them into the frame.  A slot's previous frame is
+    # finished (gather waited on, assembled) before the slot's buffers are reused.
+    pending = [None] * F
+    nstep = [0]
+
+    def finish(k):
+        work, pending[k] = pending[k], None
+        work.wait()   # orders streams[k] (the current stream) after the gather
+        if rank == 0:
+            rtamd.assemble_bands_device(frames[k].data_ptr(), gbufs[k].data_ptr(), cap, w, h, world,
+                                        args.band_rows, streams[k].cuda_stream)
 
     def step():
-        r.render_device(w, h, depth, flags, out.data_ptr(), tiling=tiling, stream=stream.cuda_stream)
-        if world > 1:
-            dist.gather(out, gather_list=gather, dst=0)
-            if rank == 0:
-                assemble()
+        k = nstep[0] % F
+        nstep[0] += 1
+        torch.cuda.set_stream(streams[k])
+        if pending[k] is not None:
+            finish(k)
+        r.render_device(w, h, depth, flags, outs[k].data_ptr(), tiling=tiling, stream=streams[k].cuda_stream)
+        if use_dist:
+            pending[k] = dist.gather(outs[k], gather_list=glists[k], dst=0, async_op=True)
+
+    def drain():
+        for j in range(F):
+            k = (nstep[0] + j) % F   # oldest first
+            if pending[k] is not None:
+                torch.cuda.set_stream(streams[k])
+                finish(k)
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    host_s = time.perf_counter() - t0   # host time to enqueue the steps (launch-bound if ~ elapsed)
+    drain()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    torch.cuda.set_stream(streams[0])
+
+    # check (untimed): rank 0's assembled frames equal its own one-rank render of the frame
+    frame_ok = None
+    if use_dist and rank == 0:
+        full = torch.zeros(h * w, dtype=torch.int32, device=dev)
+        r.render_device(w, h, depth, flags, full.data_ptr(), stream=streams[0].cuda_stream)
+        torch.cuda.synchronize(dev)
+        frame_ok = all(bool(torch.equal(full, f)) for f in frames)
 
     # per-launch kernel times of the timed steps, from the HIP events the library
     # records on the launch stream around each frame's kernels (ring of 64 frames)
     frame_ms_avg, kernel_ms_avg = r.timing_average(min(args.steps, 64))
 
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed, float(rays_local), float(prim_local)], dtype=torch.float64, device=dev)
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -207,23 +267,31 @@ def main():
     npix_sample = int(min(w * h, max(1000, budget / max(per_px, 1e-9))))
     stride = max(1, (w * h) // npix_sample)
     npix_sample = (w * h) // stride
+    # the sample is repeated (whole frames when the frame is cheaper than the budget)
+    # until about `budget` seconds of CPU work have been timed
     t0 = time.perf_counter()
-    samp = oracle.render(scene, params, w, h, depth=depth, flags=flags, pixels=(0, npix_sample, stride),
-                         nthreads=ncores, aux=False)
-    cpu_s = time.perf_counter() - t0
+    reps = 0
+    while True:
+        samp = oracle.render(scene, params, w, h, depth=depth, flags=flags, pixels=(0, npix_sample, stride),
+                             nthreads=ncores, aux=False)
+        reps += 1
+        cpu_s = time.perf_counter() - t0
+        if cpu_s >= 0.6 * budget or reps >= 1000:
+            break
     st = samp["stats"]
     cpu_rays = sum(st[k]["rays"] for k in ("primary", "shadow", "secondary"))
     kinds = [k for k in ("primary", "shadow", "secondary") if st[k]["rays"]]
     tot_bytes = sum(80.0 * st[k]["inner"] + 16.0 * st[k]["leaf"] + 64.0 * st[k]["tris"] for k in kinds)
     bpr = tot_bytes / max(1, cpu_rays)
     if world == 1 and not args.no_cpu_baseline:
-        cpu = {"value": cpu_rays / cpu_s / 1e6, "unit": "Mrays/s", "cores": ncores, "kind": "port",
+        cpu = {"value": cpu_rays * reps / cpu_s / 1e6, "unit": "Mrays/s", "cores": ncores, "kind": "port",
                "sample": f"oracle/rt_oracle.c on every {stride}th pixel of the same frame ({npix_sample} px, "
-                         f"{cpu_rays} rays, {cpu_s:.1f} s, {ncores} threads)"}
+                         f"{cpu_rays} rays) x {reps} repetition(s), {cpu_s:.1f} s, {ncores} threads"}
 
     # algorithmic bytes per launch = rays this launch traces x bytes/ray + 4 B/pixel output
     launch_rays = rays_total / max(1, world)
-    launch_bytes = launch_rays * bpr + 4.0 * (w * h) / max(1, world)
+    launch_px = (w * h) / world if world > 1 else npx
+    launch_bytes = launch_rays * bpr + 4.0 * launch_px
     achieved = launch_bytes / (kernel_ms_avg * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
@@ -249,8 +317,10 @@ def main():
         "config": {"workload": cfg["desc"], "config": args.config, "triangles": mesh.num_triangles,
                    "bvh_nodes": int(bvh.nodes.shape[0]), "width": w, "height": h, "depth": depth,
                    "shadow": not (flags & 1), "rays_per_frame": int(rays_total),
-                   "primary_rays_per_frame": int(prim_total), "parallelism": f"screen bands x{world} (RCCL gather)",
-                   "band_rows": args.band_rows, "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)"
+                   "primary_rays_per_frame": int(prim_total), "parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
+                                   else f"shard {args.shard} of the band split (diagnostic, no gather)"),
+                   "band_rows": args.band_rows, "frames_in_flight": F,
+                   "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4), "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)"
                                                         if args.bvh == "sbvh" else "binned SAH"),
                    "bvh_refs": int(bvh.tri_indices.size), "bvh_build_s": round(build_s, 3),
                    "scene_source": "Collada (rt_mesh_load_dae)" if (cfg.get("dae", True) and not args.direct)
@@ -263,8 +333,10 @@ def main():
                                 else "rtk_strict::render_kernel<true>")},
         "cpu_baseline": cpu,
     }
+    if frame_ok is not None:
+        res["config"]["gathered_frame_equals_single_rank_render"] = frame_ok
     print(json.dumps(res))
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -150,6 +150,15 @@ int rt_render_device(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_
 /* Number of pixels a rank owns under `tiling` (size of its output buffer). */
 int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* tiling);
 
+/* Rank 0 after the per-frame gather: re-interleaves the ranks'
+ * band buffers into the frame in ONE kernel launch on `stream`.  d_slots holds
+ * nranks buffers of slot_pixels pixels each (rank r's at d_slots + r*slot_pixels,
+ * its bands in the rt_tiling order); d_frame receives w*h pixels.  Replaces the
+ * single-device readback target of RayTracer.cpp:343 (the frame the reference
+ * hands to glDrawPixels).  Asynchronous: returns after enqueue. */
+int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint32_t w, uint32_t h,
+                      int32_t nranks, int32_t band_rows, void* stream);
+
 /* Kernel-side timing of the last render, from HIP events on the launch stream
  * (ms): total_ms = every kernel of the frame (counter reset / block-order
  * build, the first-bounce or fused render kernel, further bounces);

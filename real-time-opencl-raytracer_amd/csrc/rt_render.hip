@@ -211,20 +211,31 @@ struct rt_ctx {
     int32_t* d_hits = nullptr; size_t hits_cap = 0;
     float* d_t = nullptr; size_t t_cap = 0;
     float* d_rgb = nullptr; size_t rgb_cap = 0;
-    uint32_t* d_gstack = nullptr; size_t gstack_cap = 0;   // in pixels
     unsigned long long* d_overflow = nullptr;
-    // pipelined path buffers (per local pixel) + persistent grid sizes
-    float4* d_wq[2] = {nullptr, nullptr}; size_t wq_cap[2] = {0, 0};   // wavefront ray queues (ping-pong)
-    uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // frame counters (kCounters)
-    uint32_t* d_sort[4] = {nullptr, nullptr, nullptr, nullptr}; size_t sort_cap[4] = {0, 0, 0, 0};
-    uint8_t* d_sort_tmp = nullptr; size_t sort_tmp_cap = 0;
+    // Per-stream frame scratch.  Frames enqueued on different streams may run
+    // concurrently (frames in flight); each stream gets its own global stack,
+    // frame counters, wavefront queues and adaptive-order state.  Frames on one
+    // stream are ordered by it and share one slot.
+    struct FrameSlot {
+        void* stream = nullptr;
+        uint64_t last_use = 0;
+        uint32_t* d_gstack = nullptr; size_t gstack_cap = 0;                // in pixels
+        float4* d_wq[2] = {nullptr, nullptr}; size_t wq_cap[2] = {0, 0};   // wavefront ray queues (ping-pong)
+        uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // frame counters (kCounters)
+        uint32_t* d_sort[4] = {nullptr, nullptr, nullptr, nullptr}; size_t sort_cap[4] = {0, 0, 0, 0};
+        uint8_t* d_sort_tmp = nullptr; size_t sort_tmp_cap = 0;
+        uint32_t* d_cost = nullptr; size_t cost_cap = 0;   // adaptive order: last frame's per-tile times
+        uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;     //   and the longest-first order built from them
+        uint64_t cost_key = 0; bool cost_ready = false;
+    };
+    static constexpr int kMaxSlots = 8;
+    std::vector<FrameSlot> slots;
+    FrameSlot* last_slot = nullptr;
+    uint64_t slot_clock = 0;
     uint32_t* d_rank = nullptr;                                         // triangle -> first leaf position
     uint32_t* d_wt = nullptr; size_t wt_cap = 0;             // RTK_WAVE_TIMES
     uint32_t* d_order = nullptr; size_t order_cap = 0;        // tile order table for the fused kernel
     uint32_t order_tx = 0, order_ty = 0; int order_policy = -1;
-    uint32_t* d_cost = nullptr; size_t cost_cap = 0;          // adaptive order: last frame's per-tile times
-    uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;            //   and the longest-first order built from them
-    uint64_t cost_key = 0; bool cost_ready = false;
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[2] = {0, 0};   // persistent wavefront grid [strict, hw]
     int fb_grid[2] = {0, 0};   // persistent first_bounce_kernel grid [strict, hw]
@@ -269,6 +280,38 @@ static hipError_t rtk_sort_temp_bytes(int n, size_t& bytes) {
 static hipError_t rtk_sort_pairs(uint8_t* tmp, size_t bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
                                  uint32_t* vout, int n, hipStream_t s) {
     return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, 32, s);
+}
+
+static void free_slot(rt_ctx::FrameSlot& f) {
+    for (void* p : {(void*)f.d_gstack, (void*)f.d_wq[0], (void*)f.d_wq[1], (void*)f.d_wcnt, (void*)f.d_sort[0],
+                    (void*)f.d_sort[1], (void*)f.d_sort[2], (void*)f.d_sort[3], (void*)f.d_sort_tmp, (void*)f.d_cost,
+                    (void*)f.d_lpt})
+        if (p) (void)hipFree(p);
+    f = rt_ctx::FrameSlot{};
+}
+
+// The frame scratch of `stream` (created on first use; beyond kMaxSlots streams the
+// least recently used slot is recycled after its stream has drained).
+static rt_ctx::FrameSlot* slot_for(rt_ctx* c, void* stream) {
+    ++c->slot_clock;
+    for (auto& f : c->slots)
+        if (f.stream == stream) { f.last_use = c->slot_clock; return &f; }
+    if ((int)c->slots.size() < rt_ctx::kMaxSlots) {
+        c->slots.reserve(rt_ctx::kMaxSlots);   // slot pointers stay valid
+        c->slots.emplace_back();
+        c->slots.back().stream = stream;
+        c->slots.back().last_use = c->slot_clock;
+        return &c->slots.back();
+    }
+    rt_ctx::FrameSlot* lru = &c->slots[0];
+    for (auto& f : c->slots)
+        if (f.last_use < lru->last_use) lru = &f;
+    (void)hipStreamSynchronize((hipStream_t)lru->stream);
+    lru->stream = stream;
+    lru->cost_key = 0;
+    lru->cost_ready = false;
+    lru->last_use = c->slot_clock;
+    return lru;
 }
 
 static void free_scene(rt_ctx* c) {
@@ -324,9 +367,48 @@ static std::vector<uint32_t> tile_order_table(uint32_t tx, uint32_t ty, int poli
     return order;
 }
 
+// Band re-interleave on rank 0 (rt_assemble_bands): one block per frame row,
+// 16-B copies when rows and slots are 16-B aligned.  Pure HBM copy: 8 B/pixel.
+__global__ void __launch_bounds__(256) assemble_bands_kernel(uint32_t* __restrict__ frame,
+                                                             const uint32_t* __restrict__ slots, uint64_t slot_pixels,
+                                                             uint32_t w, uint32_t h, uint32_t nranks,
+                                                             uint32_t band_rows) {
+    const uint32_t y = blockIdx.x;
+    if (y >= h) return;
+    const uint32_t band = y / band_rows;
+    const uint32_t rank = band % nranks;
+    const uint64_t local_row = (uint64_t)(band / nranks) * band_rows + (y % band_rows);
+    const uint32_t* src = slots + (uint64_t)rank * slot_pixels + local_row * w;
+    uint32_t* dst = frame + (uint64_t)y * w;
+    if ((w & 3u) == 0 && (slot_pixels & 3u) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
 extern "C" {
 
 int rt_abi_version(void) { return 1; }
+
+int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint32_t w, uint32_t h,
+                      int32_t nranks, int32_t band_rows, void* stream) {
+    if (!d_frame || !d_slots || w == 0 || h == 0 || nranks < 1 || band_rows < 1)
+        return set_err(nullptr, "rt_assemble_bands: invalid argument", RT_ERR_INVALID_ARG);
+    // every rank's bands must fit its slot (rt_tiling_pixels of the fullest rank)
+    rt_tiling t0{0, nranks, band_rows, 0};
+    if ((uint64_t)rt_tiling_pixels(w, h, &t0) > slot_pixels)
+        return set_err(nullptr, "rt_assemble_bands: slot_pixels smaller than rank 0's bands", RT_ERR_INVALID_ARG);
+    if (((uintptr_t)d_frame | (uintptr_t)d_slots) & 15u)
+        return set_err(nullptr, "rt_assemble_bands: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
+    hipLaunchKernelGGL(assemble_bands_kernel, dim3(h), dim3(256), 0, (hipStream_t)stream, d_frame, d_slots,
+                       slot_pixels, w, h, (uint32_t)nranks, (uint32_t)band_rows);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(nullptr, std::string("rt_assemble_bands: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    return RT_OK;
+}
 
 const char* rt_last_error(rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
@@ -359,12 +441,10 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_hits) (void)hipFree(c->d_hits);
     if (c->d_t) (void)hipFree(c->d_t);
     if (c->d_rgb) (void)hipFree(c->d_rgb);
-    if (c->d_gstack) (void)hipFree(c->d_gstack);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
-    for (void* p : {(void*)c->d_wq[0], (void*)c->d_wq[1], (void*)c->d_wcnt, (void*)c->d_sort[0],
-                    (void*)c->d_sort[1], (void*)c->d_sort[2], (void*)c->d_sort[3], (void*)c->d_sort_tmp,
-                    (void*)c->d_order, (void*)c->d_wt,
-                    (void*)c->d_cost, (void*)c->d_lpt})
+    (void)hipDeviceSynchronize();   // frames may still run on caller streams
+    for (auto& f : c->slots) free_slot(f);
+    for (void* p : {(void*)c->d_order, (void*)c->d_wt})
         if (p) (void)hipFree(p);
     for (auto& f : c->ring)
         for (hipEvent_t& e : f.e)
@@ -556,6 +636,8 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     if (npix == 0) return RT_OK;
     int rc = RT_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    rt_ctx::FrameSlot& L = *slot_for(c, (void*)s);
+    c->last_slot = &L;
 
     rtk::Frame F;
     const rt_params& P = c->params;
@@ -593,7 +675,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.hits = aux ? d_aux->hits : nullptr;
     O.t = aux ? d_aux->t : nullptr;
     O.rgb = aux ? d_aux->rgb : nullptr;
-    O.gstack = c->d_gstack;
+    O.gstack = L.d_gstack;
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
     O.wave_times = nullptr;
@@ -607,12 +689,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     // the fused kernel specialised to a single bounce
     const bool wavefront = ((flags & RT_FLAG_WAVEFRONT) && depth > 0) || depth == 1;
 
-    if ((rc = ensure(c, c->d_gstack, c->gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
-    O.gstack = c->d_gstack;
+    if ((rc = ensure(c, L.d_gstack, L.gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
+    O.gstack = L.d_gstack;
     // frame counters: [8k + 0] queue size of bounce k, [8k + 2] its fetch cursor,
     // [kRestartSlot] restarted traversals; zeroed by the frame's first launch
-    if ((rc = ensure(c, c->d_wcnt, c->wcnt_cap, kCounters))) return rc;
-    O.restarts = c->d_wcnt + kRestartSlot;
+    if ((rc = ensure(c, L.d_wcnt, L.wcnt_cap, kCounters))) return rc;
+    O.restarts = L.d_wcnt + kRestartSlot;
 #if RTK_WAVE_TIMES
     if (std::getenv("RTAMD_WAVE_TIMES")) {
         if ((rc = ensure(c, c->d_wt, c->wt_cap, (size_t)npix * 4))) return rc;
@@ -642,18 +724,18 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.tile_cost = nullptr;
     bool lpt = false;
     if (!(flags & RT_FLAG_STATIC_ORDER)) {
-        if ((rc = ensure(c, c->d_cost, c->cost_cap, units))) return rc;
-        if ((rc = ensure(c, c->d_lpt, c->lpt_cap, units))) return rc;
+        if ((rc = ensure(c, L.d_cost, L.cost_cap, units))) return rc;
+        if ((rc = ensure(c, L.d_lpt, L.lpt_cap, units))) return rc;
         const uint64_t key = ((uint64_t)F.tiles_x << 48) ^ ((uint64_t)F.tiles_y << 32) ^ F.local_rows ^
                              ((uint64_t)c->scene_gen << 20) ^ (wavefront ? (1ull << 63) : 0ull) ^
                              (persistent ? (1ull << 62) : 0ull);
-        if (key != c->cost_key) {
-            HIPC(c, hipMemsetAsync(c->d_cost, 0, (size_t)units * 4, s));
-            c->cost_key = key;
-            c->cost_ready = false;
+        if (key != L.cost_key) {
+            HIPC(c, hipMemsetAsync(L.d_cost, 0, (size_t)units * 4, s));
+            L.cost_key = key;
+            L.cost_ready = false;
         }
-        lpt = c->cost_ready;
-        F.tile_cost = c->d_cost;
+        lpt = L.cost_ready;
+        F.tile_cost = L.d_cost;
     }
     const bool fast_kernel = S.clean != 0;   // any quotient domain: traverse_fast picks the variant
     const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES);
@@ -661,11 +743,11 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     HIPC(c, hipEventRecord(E.e[0], s));
     // first launch: zero the counters (all of them for the wavefront queues, else the
     // restart count) and, with a measured previous frame, build the longest-first order
-    hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, c->d_cost, c->d_lpt,
-                       lpt ? units : 0u, wavefront ? c->d_wcnt : c->d_wcnt + kRestartSlot,
+    hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, L.d_cost, L.d_lpt,
+                       lpt ? units : 0u, wavefront ? L.d_wcnt : L.d_wcnt + kRestartSlot,
                        wavefront ? (uint32_t)kCounters : 1u);
-    if (lpt) F.tile_order = c->d_lpt;
-    if (F.tile_cost) c->cost_ready = true;
+    if (lpt) F.tile_order = L.d_lpt;
+    if (F.tile_cost) L.cost_ready = true;
 
     if (!wavefront) {
         HIPC(c, hipEventRecord(E.e[2], s));
@@ -693,18 +775,18 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             c->wf_grid[mi] = std::max(8, std::max(b1, 1) * cus);
         }
         const size_t qcap = (size_t)npix * 3;  // float4 per QRay x 3
-        if (depth > 1 && (rc = ensure(c, c->d_wq[0], c->wq_cap[0], qcap))) return rc;
-        if (depth > 1 && (rc = ensure(c, c->d_wq[1], c->wq_cap[1], qcap))) return rc;
+        if (depth > 1 && (rc = ensure(c, L.d_wq[0], L.wq_cap[0], qcap))) return rc;
+        if (depth > 1 && (rc = ensure(c, L.d_wq[1], L.wq_cap[1], qcap))) return rc;
         const bool sort = (flags & RT_FLAG_WF_SORT) && depth > 1 && c->d_rank;
         if (sort) {
             for (int i = 0; i < 4; ++i)
-                if ((rc = ensure(c, c->d_sort[i], c->sort_cap[i], (size_t)npix))) return rc;
+                if ((rc = ensure(c, L.d_sort[i], L.sort_cap[i], (size_t)npix))) return rc;
             size_t need = 0;
             HIPC(c, rtk_sort_temp_bytes((int)npix, need));
-            if ((rc = ensure(c, c->d_sort_tmp, c->sort_tmp_cap, need))) return rc;
+            if ((rc = ensure(c, L.d_sort_tmp, L.sort_tmp_cap, need))) return rc;
         }
-        auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)c->d_wq[k & 1] : (rtk::QRay*)nullptr; };
-        uint32_t* cnt = c->d_wcnt;
+        auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)L.d_wq[k & 1] : (rtk::QRay*)nullptr; };
+        uint32_t* cnt = L.d_wcnt;
         dim3 fgrid = grid;
         if (persistent) {
             if (!c->fb_grid[mi]) {
@@ -743,11 +825,11 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.perm = nullptr;
             if (sort) {
                 hipLaunchKernelGGL(rtk_strict::wf_key_kernel, dim3(1024), dim3(256), 0, s,
-                                   (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, c->d_sort[0],
-                                   c->d_sort[1], c->d_rank);
-                HIPC(c, rtk_sort_pairs(c->d_sort_tmp, c->sort_tmp_cap, c->d_sort[0], c->d_sort[2], c->d_sort[1],
-                                       c->d_sort[3], (int)npix, s));
-                W.perm = c->d_sort[3];
+                                   (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, L.d_sort[0],
+                                   L.d_sort[1], c->d_rank);
+                HIPC(c, rtk_sort_pairs(L.d_sort_tmp, L.sort_tmp_cap, L.d_sort[0], L.d_sort[2], L.d_sort[1],
+                                       L.d_sort[3], (int)npix, s));
+                W.perm = L.d_sort[3];
             }
             W.out = qbuf(k + 1);
             W.out_count = cnt + 8 * (k + 1) + 0;
@@ -850,9 +932,9 @@ int rt_timing_average(rt_ctx* c, int32_t n, float* total_ms, float* traverse_ms)
 int rt_last_deferred(rt_ctx* c, uint32_t* count) {
     if (!c || !count) return RT_ERR_INVALID_ARG;
     *count = 0;
-    if (!c->d_wcnt) return RT_OK;
-    HIPC(c, hipStreamSynchronize(c->stream));
-    HIPC(c, hipMemcpy(count, c->d_wcnt + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (!c->last_slot || !c->last_slot->d_wcnt) return RT_OK;
+    HIPC(c, hipStreamSynchronize((hipStream_t)c->last_slot->stream));
+    HIPC(c, hipMemcpy(count, c->last_slot->d_wcnt + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

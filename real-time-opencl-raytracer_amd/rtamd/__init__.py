@@ -80,7 +80,7 @@ class rt_bvh_view(C.Structure):
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
 ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_device",
-               "rt_tiling_pixels", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_tiling_pixels", "rt_assemble_bands", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
@@ -114,6 +114,7 @@ def lib() -> C.CDLL:
             "rt_render": (C.c_int, [vp, u32, u32, i32, u32, vp, C.POINTER(rt_aux)]),
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
             "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
+            "rt_assemble_bands": (C.c_int, [vp, vp, C.c_uint64, u32, u32, i32, i32, vp]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
             "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
             "rt_last_deferred": (C.c_int, [vp, C.POINTER(u32)]),
@@ -424,7 +425,11 @@ class Renderer:
         return out
 
     def render_device(self, w, h, depth, flags, d_out_ptr: int, tiling: Optional[rt_tiling] = None,
-                      stream: int = 0, aux_ptrs=None):
+                      stream: Optional[int] = None, aux_ptrs=None):
+        """Enqueue a frame on `stream` (a hipStream_t handle, e.g. torch.cuda.Stream().cuda_stream);
+        None = the ctx's own stream.  torch's default stream (handle 0) is refused: the C ABI reads
+        NULL as the ctx stream, which does not order with the legacy null stream."""
+        _stream_arg(stream)
         ax = None if aux_ptrs is None else C.byref(rt_aux(*aux_ptrs))
         _check(lib().rt_render_device(self._h, w, h, depth, flags, None if tiling is None else C.byref(tiling),
                                       C.c_void_p(d_out_ptr), ax, C.c_void_p(stream or None)), self._h)
@@ -471,19 +476,34 @@ def rank_bands(h: int, rank: int, nranks: int, band_rows: int):
     return [(b * band_rows, min(band_rows, h - b * band_rows)) for b in range(rank, nbands, nranks)]
 
 
+def _stream_arg(stream):
+    if stream is not None and int(stream) == 0:
+        raise ValueError("stream 0 (the null stream) is not accepted: the C ABI reads NULL as the ctx stream; "
+                         "run under a torch.cuda.Stream")
+
+
+def assemble_bands_device(d_frame: int, d_slots: int, slot_pixels: int, w: int, h: int, nranks: int,
+                          band_rows: int, stream: int) -> None:
+    """rt_assemble_bands: rank 0's band re-interleave as one HIP launch on `stream`
+    (device pointers; d_slots = nranks equal slots of slot_pixels pixels)."""
+    _stream_arg(stream)
+    _check(lib().rt_assemble_bands(C.c_void_p(d_frame), C.c_void_p(d_slots), slot_pixels, w, h, nranks, band_rows,
+                                   C.c_void_p(stream or None)))
+
+
 def assemble_bands(frame, chunks, w: int, h: int, band_rows: int):
-    """Re-interleave gathered per-rank band buffers into the frame (rank 0 after the
-    gather).  `frame` is (h*w,) and chunks[r] holds rank r's bands in order; works on
-    numpy arrays and on torch tensors (device copies stay on the device)."""
+    """Host restatement of rt_assemble_bands (tests): re-interleave per-rank band
+    buffers into the frame.  `frame` is (h*w,) and chunks[r] holds rank r's bands in
+    order (it may be longer than the bands, e.g. a padded gather slot); numpy arrays
+    or torch tensors (device copies stay on the device)."""
     nranks = len(chunks)
-    fv = frame.reshape(h, w) if hasattr(frame, "reshape") else frame.view(h, w)
     for r, ch in enumerate(chunks):
-        src = ch.reshape(-1, w) if not hasattr(ch, "view") or isinstance(ch, np.ndarray) else ch.view(-1, w)
         row = 0
         for y0, n in rank_bands(h, r, nranks, band_rows):
-            if isinstance(fv, np.ndarray):
-                fv[y0:y0 + n] = src[row:row + n]
+            dst, src = frame[y0 * w:(y0 + n) * w], ch[row * w:(row + n) * w]
+            if isinstance(frame, np.ndarray):
+                dst[:] = src
             else:
-                fv[y0:y0 + n].copy_(src[row:row + n], non_blocking=True)
+                dst.copy_(src, non_blocking=True)
             row += n
     return frame

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wave_times.bin"))
+    ap.add_argument("--shard", default="", help="R/N: one rank's bands of an N-way split (8-row bands)")
     args = ap.parse_args()
     import torch
     import bench
@@ -31,18 +32,24 @@ def main():
     r = rtamd.Renderer(0)
     r.upload(scene)
     r.set_params(rtamd.params_to_array(mesh.camera_params(w, h)))
-    out = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    tiling = None
+    hl = h
+    if args.shard:
+        sr, sn = (int(v) for v in args.shard.split("/"))
+        tiling = rtamd.rt_tiling(sr, sn, 8, 0)
+        hl = rtamd.tiling_pixels(w, h, sr, sn, 8) // w
+    out = torch.zeros(w * hl, dtype=torch.int32, device="cuda")
     for _ in range(3):
-        r.render_device(w, h, cfg["depth"], cfg["flags"], out.data_ptr())
+        r.render_device(w, h, cfg["depth"], cfg["flags"], out.data_ptr(), tiling=tiling)
     torch.cuda.synchronize()
     os.environ["RTAMD_WAVE_TIMES"] = args.out
-    r.render_device(w, h, cfg["depth"], cfg["flags"], out.data_ptr())
+    r.render_device(w, h, cfg["depth"], cfg["flags"], out.data_ptr(), tiling=tiling)
     torch.cuda.synchronize()
     print("kernel ms (with stamps):", r.last_kernel_ms())
 
     wt = np.fromfile(args.out, dtype=np.uint32).reshape(-1, 4)
     # pixel -> wave: 8x8 tiles (lane = pixel in the tile)
-    px = np.arange(w * h)
+    px = np.arange(w * hl)
     x, y = px % w, px // w
     wave = (y // 8) * ((w + 7) // 8) + (x // 8)
     t0 = wt[:, 0].astype(np.int64)
@@ -71,6 +78,13 @@ def main():
     print(f"last wave start at {ws.max() * tick_ns / 1e3:.1f} us; tail after it {(end - ws.max()) * tick_ns / 1e3:.1f} us")
     print(f"wave duration us: mean {wave_len.mean() * tick_ns / 1e3:.2f} p50 {np.median(wave_len) * tick_ns / 1e3:.2f} "
           f"p90 {np.percentile(wave_len, 90) * tick_ns / 1e3:.2f} max {wave_len.max() * tick_ns / 1e3:.2f}")
+    pc = np.percentile(wave_len, [1, 10, 25, 50, 75, 90, 99, 99.9]) * tick_ns / 1e3
+    print("wave duration percentiles 1/10/25/50/75/90/99/99.9 (us):", " ".join(f"{v:.1f}" for v in pc))
+    top = np.argsort(wave_len)[-8:][::-1]
+    tx = (w + 7) // 8
+    print("longest waves (tile x, local tile row, us, lane util):",
+          "; ".join(f"({t % tx},{t // tx}) {wave_len[t] * tick_ns / 1e3:.1f} {lane_sum[t] / (64 * max(wave_len[t], 1)):.2f}"
+                    for t in top))
     print(f"lane utilisation inside waves (time-weighted): {lane_sum.sum() / (64 * wave_len.sum()):.3f}")
     # resident waves over time
     nb = 50

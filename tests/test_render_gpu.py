@@ -100,7 +100,7 @@ def test_band_tiling_reassembles(renderer, nranks, band_rows):
         npx = rtamd.tiling_pixels(w, h, rank, nranks, band_rows)
         buf = torch.zeros(max(npx, 1), dtype=torch.int32, device="cuda")
         t = rtamd.rt_tiling(rank, nranks, band_rows, 0)
-        renderer.render_device(w, h, 1, 0, buf.data_ptr(), tiling=t, stream=torch.cuda.current_stream().cuda_stream)
+        renderer.render_device(w, h, 1, 0, buf.data_ptr(), tiling=t)   # the ctx's own stream
         torch.cuda.synchronize()
         local = buf.cpu().numpy().view(np.uint32)[:npx].reshape(-1, w)
         row = 0
@@ -109,6 +109,43 @@ def test_band_tiling_reassembles(renderer, nranks, band_rows):
             img[b * band_rows:b * band_rows + n] = local[row:row + n]
             row += n
     assert np.array_equal(img.reshape(-1), full)
+
+
+@pytest.mark.parametrize("nranks,band_rows,w", [(2, 16, 0), (3, 8, 0), (8, 8, 0), (5, 8, 123)])
+def test_device_band_assembly(renderer, nranks, band_rows, w):
+    """bench.py's multi-GPU frame path on one device: every rank's bands rendered into
+    its slot of one (nranks, slot) buffer -- what the RCCL gather delivers to rank 0 --
+    then rt_assemble_bands re-interleaves them; the frame equals a one-rank render.
+    w = 123 takes the unaligned (4-byte) copy path."""
+    import rtamd
+    import torch
+    d = load_golden("hf40k")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w = w or int(d["w"])
+    h = int(d["h"]) - 8  # a short last band
+    full = renderer.render(w, h, depth=1)
+    slot = rtamd.tiling_pixels(w, h, 0, nranks, band_rows)
+    slot = (slot + 3) // 4 * 4
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):   # bench.py's setting: every launch on one torch side stream
+        slots = torch.full((nranks, slot), -7, dtype=torch.int32, device="cuda")
+        frame = torch.full((h * w,), -9, dtype=torch.int32, device="cuda")
+        s = side.cuda_stream
+        for rank in range(nranks):
+            t = rtamd.rt_tiling(rank, nranks, band_rows, 0)
+            renderer.render_device(w, h, 1, 0, slots[rank].data_ptr(), tiling=t, stream=s)
+        rtamd.assemble_bands_device(frame.data_ptr(), slots.data_ptr(), slot, w, h, nranks, band_rows, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32), full)
+    # the numpy host restatement of the same re-interleave agrees
+    host = np.zeros(w * h, np.uint32)
+    rtamd.assemble_bands(host, [x.view(np.uint32) for x in slots.cpu().numpy()], w, h, band_rows)
+    assert np.array_equal(host, full)
+    with pytest.raises(rtamd.RtError):   # slot too small for rank 0's bands
+        rtamd.assemble_bands_device(frame.data_ptr(), slots.data_ptr(), slot // 2, w, h, nranks, band_rows, s)
+    with pytest.raises(ValueError):      # the null stream is refused (NULL = ctx stream in the ABI)
+        rtamd.assemble_bands_device(frame.data_ptr(), slots.data_ptr(), slot, w, h, nranks, band_rows, 0)
 
 
 def test_errors(renderer):
