@@ -75,6 +75,12 @@
 #ifndef RTK_PERSISTENT
 #define RTK_PERSISTENT 0   // first_bounce_kernel: persistent waves over a tile counter (A/B: slower)
 #endif
+#ifndef RTK_IFIF
+#define RTK_IFIF 1          // fast traversal: lane-independent steps (traverse_ifif) instead of while-while
+#endif
+#ifndef RTK_TRI_PIPE
+#define RTK_TRI_PIPE 1      // fast traversal: next triangle record in flight while the current one is tested
+#endif
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
 #endif
@@ -554,7 +560,8 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             }
         }
         // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974)
-        std::vector<float4> tr((size_t)std::max(nref, 1) * 3, make_float4(0, 0, 0, 0));
+        // + a 16-B tail pad: traverse_ifif fetches 64 B at a triangle record (48 B used)
+        std::vector<float4> tr((size_t)std::max(nref, 1) * 3 + 1, make_float4(0, 0, 0, 0));
         for (int32_t i = 0; i < nref; ++i) {
             const int32_t tri1 = refs[i];
             const rt_float4 v0 = verts[idx[tri1]], v1 = verts[idx[tri1 + 1]], v2 = verts[idx[tri1 + 2]];
