@@ -78,6 +78,9 @@
 #ifndef RTK_IFIF
 #define RTK_IFIF 1          // fast traversal: lane-independent steps (traverse_ifif) instead of while-while
 #endif
+#ifndef RTK_NODE_CACHE
+#define RTK_NODE_CACHE 0    // depth-1 fast kernel: inner records (BFS top) copied into each block's LDS (A/B: slower)
+#endif
 #ifndef RTK_TRI_PIPE
 #define RTK_TRI_PIPE 1      // fast traversal: next triangle record in flight while the current one is tested
 #endif
@@ -102,6 +105,7 @@ struct DevScene {
     const float4* __restrict__ shade;    // [n_tris][7]
     const int2* __restrict__ leaf_table; // escape leaves {offset, count}
     uint32_t root;
+    uint32_t n_inner;                    // inner records; the first ones are the BVH's top levels (BFS order)
     int fast_div;                        // every box coordinate is 0 or in [2^-66, 2^60]
     int clean;                           // no reachable malformed inner node (kRefError)
 };
@@ -164,6 +168,8 @@ struct Stack {
     uint32_t* lds;      // this lane's column: lds[i * 64]
     uint32_t* glb;      // this pixel's column: glb[(i - kLdsStack) * gstride]
     uint64_t gstride;
+    const float4* nc = nullptr;   // LDS copy of inner records 0 .. ncn-1 (fast traversal), or none
+    uint32_t ncn = 0;
     __device__ __forceinline__ uint32_t get(int i) const {
         return i < kLdsStack ? lds[i * 64] : glb[(uint64_t)(i - kLdsStack) * gstride];
     }
@@ -208,6 +214,7 @@ struct rt_ctx {
     float4* d_shade = nullptr;
     int2* d_leaf = nullptr;
     uint32_t root = 0;
+    uint32_t n_inner = 0;
     int fast_div = 0;
     int clean = 0;
     bool have_scene = false;
@@ -512,6 +519,30 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             state[n] = 2;
             stk.pop_back();
         }
+        // Renumber: the first kBfsTop inner nodes in breadth-first order from the root get
+        // ids 0..kBfsTop-1 (the top of the tree, which every ray walks: the fast kernel keeps
+        // the first RTK_NODE_CACHE of them in LDS); the rest keep their pre-order.
+        {
+            constexpr int32_t kBfsTop = 1024;
+            std::vector<int32_t> bfs;
+            std::vector<uint8_t> seen(nn, 0);
+            if (inner_id[0] >= 0) { bfs.push_back(0); seen[0] = 1; }
+            for (size_t i = 0; i < bfs.size() && (int32_t)bfs.size() < kBfsTop; ++i) {
+                const rt_bvh_node& nd = nodes[bfs[i]];
+                for (int32_t ch : {nd.offset_left, nd.offset_right})
+                    if (inner_id[ch] >= 0 && !seen[ch] && (int32_t)bfs.size() < kBfsTop) {
+                        seen[ch] = 1;
+                        bfs.push_back(ch);
+                    }
+            }
+            std::vector<int32_t> by_old(next, -1);
+            for (int32_t n = 0; n < nn; ++n)
+                if (inner_id[n] >= 0) by_old[inner_id[n]] = n;
+            int32_t id = 0;
+            for (int32_t n : bfs) inner_id[n] = id++;
+            for (int32_t o = 0; o < next; ++o)
+                if (!seen[by_old[o]]) inner_id[by_old[o]] = id++;
+        }
         bool clean = true;
         for (int32_t n = 0; n < nn; ++n)
             if (state[n] != 0 && nodes[n].offset_left >= 0 && inner_id[n] < 0) clean = false;
@@ -603,6 +634,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         HIPC(c, hipMemcpy(c->d_shade, sh.data(), sh.size() * sizeof(float4), hipMemcpyHostToDevice));
         HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
         c->root = ref_of[0];
+        c->n_inner = (uint32_t)n_inner;
         c->fast_div = fast_ok ? 1 : 0;
         c->have_scene = true;
         ++c->scene_gen;
@@ -675,7 +707,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.tile_order = nullptr;
     F.tile_cost = nullptr;
 
-    rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root,
+    rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root, c->n_inner,
                     (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0, c->clean};
     rtk::Outputs O;
     O.out = d_out;
@@ -799,9 +831,9 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             if (!c->fb_grid[mi]) {
                 int cus = 0, b1 = 0;
                 HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-                if (hw) HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_hw::first_bounce_kernel<true>,
+                if (hw) HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (rtk_hw::first_bounce_kernel<true, true>),
                                                                              64 * RTK_FUSED_WAVES, 0));
-                else HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_strict::first_bounce_kernel<true>,
+                else HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (rtk_strict::first_bounce_kernel<true, true>),
                                                                           64 * RTK_FUSED_WAVES, 0));
                 c->fb_grid[mi] = std::max(1, b1) * cus;
             }
@@ -814,14 +846,19 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.out = qbuf(1);
             W.out_count = cnt + 8 * 1 + 0;
             W.bounce = 0;
+            // <FASTONLY, NEXT>: NEXT parks the next bounce's ray (depth > 1); a depth-1 frame's
+            // fast kernel holds the top of the BVH in LDS instead
+#define RTK_FB(NS, FAST, NEXT) hipLaunchKernelGGL((NS::first_bounce_kernel<FAST, NEXT>), fgrid, block, 0, s, S, F, O, W, ax)
+            const bool nx = depth > 1;
             if (fast_kernel) {
-                if (hw) hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<true>, fgrid, block, 0, s, S, F, O, W, ax);
-                else hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<true>, fgrid, block, 0, s, S, F, O, W, ax);
+                if (hw) { if (nx) RTK_FB(rtk_hw, true, true); else RTK_FB(rtk_hw, true, false); }
+                else { if (nx) RTK_FB(rtk_strict, true, true); else RTK_FB(rtk_strict, true, false); }
             } else if (hw) {
-                hipLaunchKernelGGL(rtk_hw::first_bounce_kernel<false>, fgrid, block, 0, s, S, F, O, W, ax);
+                RTK_FB(rtk_hw, false, true);
             } else {
-                hipLaunchKernelGGL(rtk_strict::first_bounce_kernel<false>, fgrid, block, 0, s, S, F, O, W, ax);
+                RTK_FB(rtk_strict, false, true);
             }
+#undef RTK_FB
         }
         HIPC(c, hipEventRecord(E.e[3], s));
         E.has_k = true;
