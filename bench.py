@@ -24,6 +24,13 @@ for _p in (PKG, ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+# Frames in flight run on separate streams; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
+# queues (4 by default, and exported as 4 on the GPU boxes; shared with torch's and the
+# library's own streams), so with four frames in flight two would share a queue and
+# serialise.  Raised to at least 8, before HIP starts (measured: 1/8 shard 0.075 -> 0.055 ms).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 METRIC = "Mrays/sec (primary+1 shadow) @1080p, 1M-tri SAH BVH; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # C3 terrain extent: fills the default camera's 1080p view (Camera.cpp:6-19)
@@ -82,7 +89,7 @@ def main():
     ap.add_argument("--band-rows", type=int, default=8,
                     help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
     ap.add_argument("--dist", action="store_true", help="use the process-group gather path even at N = 1")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="frames in flight (one stream each): frame i+1 renders while frame i drains / gathers")
     ap.add_argument("--shard", default="", help="R/N: render only rank R's bands of an N-way split (diagnostic)")
     ap.add_argument("--direct", action="store_true", help="skip the Collada write/read of the scene")
@@ -293,6 +300,10 @@ def main():
     launch_px = (w * h) / world if world > 1 else npx
     launch_bytes = launch_rays * bpr + 4.0 * launch_px
     achieved = launch_bytes / (kernel_ms_avg * 1e-3) / 1e9
+    # with F frames in flight the launches overlap, so a launch's duration includes the time it
+    # shares the GPU with its neighbours: the per-launch rate above under-reads the kernel's
+    # throughput by up to ~F x.  The aggregate rate is the same bytes over the wall time per frame.
+    achieved_aggregate = launch_bytes / (ms_per_step * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
     if os.path.exists(pmc_path):
@@ -320,6 +331,7 @@ def main():
                    "primary_rays_per_frame": int(prim_total), "parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
                                    else f"shard {args.shard} of the band split (diagnostic, no gather)"),
                    "band_rows": args.band_rows, "frames_in_flight": F,
+                   "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                    "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4), "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)"
                                                         if args.bvh == "sbvh" else "binned SAH"),
                    "bvh_refs": int(bvh.tri_indices.size), "bvh_build_s": round(build_s, 3),
@@ -327,9 +339,12 @@ def main():
                    else "in-memory generator"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "achieved_aggregate": round(achieved_aggregate, 2),
+                     "frac_aggregate": round(achieved_aggregate / HBM_PEAK_GBS, 4),
+                     "launches_overlap": F > 1,
                      "bytes_per_ray": round(bpr, 1), "kernel_ms": round(kernel_ms_avg, 4),
                      "frame_kernels_ms": round(frame_ms_avg, 4),
-                     "kernel": ("rtk_strict::first_bounce_kernel<true>" if depth == 1 or (flags & 8)
+                     "kernel": ("rtk_strict::first_bounce_kernel<true, false>" if depth == 1 else "rtk_strict::first_bounce_kernel<true, true>" if (flags & 8)
                                 else "rtk_strict::render_kernel<true>")},
         "cpu_baseline": cpu,
     }

@@ -782,7 +782,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     HIPC(c, hipEventRecord(E.e[0], s));
     // first launch: zero the counters (all of them for the wavefront queues, else the
     // restart count) and, with a measured previous frame, build the longest-first order
-    hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(1024), 0, s, L.d_cost, L.d_lpt,
+    hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(256), 0, s, L.d_cost, L.d_lpt,
                        lpt ? units : 0u, wavefront ? L.d_wcnt : L.d_wcnt + kRestartSlot,
                        wavefront ? (uint32_t)kCounters : 1u);
     if (lpt) F.tile_order = L.d_lpt;

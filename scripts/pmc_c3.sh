@@ -9,6 +9,7 @@ if [ $# -eq 0 ]; then
          "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
          "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_VALU" \
          "TCC_HIT_sum TCC_MISS_sum SQ_INSTS_LDS SQ_INSTS_VMEM_RD" \
+         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_INSTS_FLAT" \
          "FETCH_SIZE" "WRITE_SIZE"
 fi
 mkdir -p "$out"
@@ -16,6 +17,6 @@ i=0
 for set in "$@"; do
   i=$((i+1))
   timeout -k 10 180 rocprofv3 --pmc $set -d $out/p$i -o run --output-format csv -- \
-      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $out/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --inflight 1 > $out/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
 python3 scripts/pmc_summary.py $out/p*

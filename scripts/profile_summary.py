@@ -15,7 +15,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "first_bounce_kernel<true>"   # C3 is depth 1: the single-bounce kernel
+KERNEL = "first_bounce_kernel<true, false>"   # C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray)
 
 
 def counter(d, name):
@@ -45,7 +45,7 @@ def main():
         if os.path.exists(p):
             shutil.copy(p, os.path.join(out, f"{cfg}_{log.replace('prof_', '')}"))
     res = {
-        "config": cfg, "kernel": "rtk_strict::first_bounce_kernel<true>", "round": rnd,
+        "config": cfg, "kernel": "rtk_strict::" + KERNEL, "round": rnd,
         "rocprof_avg_kernel_us": None if avg_ns is None else round(avg_ns / 1e3, 2),
         "FETCH_SIZE_kB_median": fetch, "WRITE_SIZE_kB_median": write, "dispatches": [nf, nw],
         "correction": "FETCH_SIZE x2 (gfx950 reports half the bytes of 16B/lane reads, MI355X_MICROARCH.md HBM); "

@@ -148,6 +148,30 @@ def test_device_band_assembly(renderer, nranks, band_rows, w):
         rtamd.assemble_bands_device(frame.data_ptr(), slots.data_ptr(), slot, w, h, nranks, band_rows, 0)
 
 
+@pytest.mark.parametrize("depth", [1, 3])
+def test_frames_in_flight_on_streams(renderer, depth):
+    """Frames enqueued back to back on different streams overlap on the GPU; each stream
+    has its own frame scratch in the ctx (stack spill, counters, adaptive order), so every
+    frame equals the synchronous render (bench.py runs 4 frames in flight)."""
+    import rtamd
+    import torch
+    d = load_golden("hf40k")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    ref = renderer.render(w, h, depth=depth)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.full((w * h,), -3, dtype=torch.int32, device="cuda") for _ in range(6)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):   # two rounds over three streams, nothing waited for in between
+        renderer.render_device(w, h, depth, 0, o.data_ptr(), stream=streams[i % 3].cuda_stream)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), ref)
+    with pytest.raises(ValueError):   # torch's default stream (handle 0) is refused
+        renderer.render_device(w, h, depth, 0, outs[0].data_ptr(), stream=0)
+
+
 def test_errors(renderer):
     import rtamd
     r = rtamd.Renderer(0)
