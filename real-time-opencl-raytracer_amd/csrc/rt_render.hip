@@ -81,6 +81,9 @@
 #ifndef RTK_NODE_CACHE
 #define RTK_NODE_CACHE 0    // depth-1 fast kernel: inner records (BFS top) copied into each block's LDS (A/B: slower)
 #endif
+#ifndef RTK_SCALAR_SHARE
+#define RTK_SCALAR_SHARE 0  // traverse_ifif: first active lane's record via the scalar cache for the lanes sharing it (A/B: slower)
+#endif
 #ifndef RTK_TRI_PIPE
 #define RTK_TRI_PIPE 1      // fast traversal: next triangle record in flight while the current one is tested
 #endif
