@@ -181,13 +181,28 @@ def main():
     # finished (gather waited on, assembled) before the slot's buffers are reused.
     pending = [None] * F
     nstep = [0]
+    # the per-frame host path, with everything constant bound once: at N = 8 a frame is
+    # ~0.055 ms of GPU time, so the host's enqueue per frame has to stay well under that
+    launch = r.frame_launcher(w, h, depth, flags, tiling)
+    sh = [st.cuda_stream for st in streams]
+    out_ptr = [o.data_ptr() for o in outs]
+    if use_dist:
+        pg = dist.distributed_c10d._get_default_group()
+        gopts = dist.GatherOptions()
+        gopts.rootRank = 0
+        gopts.asyncOp = True
+        g_out = [[glists[k]] if rank == 0 else [] for k in range(F)]
+        g_in = [[o] for o in outs]
+        if rank == 0:
+            assemble = rtamd.bands_assembler(w, h, world, args.band_rows, cap)
+            frame_ptr = [f.data_ptr() for f in frames]
+            gbuf_ptr = [g.data_ptr() for g in gbufs]
 
     def finish(k):
         work, pending[k] = pending[k], None
         work.wait()   # orders streams[k] (the current stream) after the gather
         if rank == 0:
-            rtamd.assemble_bands_device(frames[k].data_ptr(), gbufs[k].data_ptr(), cap, w, h, world,
-                                        args.band_rows, streams[k].cuda_stream)
+            assemble(frame_ptr[k], gbuf_ptr[k], sh[k])
 
     def step():
         k = nstep[0] % F
@@ -195,9 +210,9 @@ def main():
         torch.cuda.set_stream(streams[k])
         if pending[k] is not None:
             finish(k)
-        r.render_device(w, h, depth, flags, outs[k].data_ptr(), tiling=tiling, stream=streams[k].cuda_stream)
-        if use_dist:
-            pending[k] = dist.gather(outs[k], gather_list=glists[k], dst=0, async_op=True)
+        launch(out_ptr[k], sh[k])
+        if use_dist:   # dist.gather(outs[k], glists[k], dst=0, async_op=True) without its argument checks
+            pending[k] = pg.gather(g_out[k], g_in[k], gopts)
 
     def drain():
         for j in range(F):

@@ -434,6 +434,20 @@ class Renderer:
         _check(lib().rt_render_device(self._h, w, h, depth, flags, None if tiling is None else C.byref(tiling),
                                       C.c_void_p(d_out_ptr), ax, C.c_void_p(stream or None)), self._h)
 
+    def frame_launcher(self, w, h, depth, flags, tiling: Optional[rt_tiling] = None):
+        """A callable (d_out_ptr, stream) -> None that enqueues one frame like render_device,
+        with its constant ctypes arguments built once (a per-frame host loop's fast path)."""
+        fn = lib().rt_render_device
+        hdl, tl = self._h, (None if tiling is None else C.byref(tiling))
+        w, h, depth, flags = C.c_uint32(w), C.c_uint32(h), C.c_int32(depth), C.c_uint32(flags)
+
+        def launch(d_out_ptr: int, stream: int) -> None:
+            _stream_arg(stream)
+            rc = fn(hdl, w, h, depth, flags, tl, d_out_ptr, None, stream)
+            if rc:
+                _check(rc, hdl)
+        return launch
+
     def last_kernel_ms(self) -> float:
         """All kernels of the last frame (ms, HIP events on the launch stream)."""
         t = C.c_float()
@@ -489,6 +503,20 @@ def assemble_bands_device(d_frame: int, d_slots: int, slot_pixels: int, w: int, 
     _stream_arg(stream)
     _check(lib().rt_assemble_bands(C.c_void_p(d_frame), C.c_void_p(d_slots), slot_pixels, w, h, nranks, band_rows,
                                    C.c_void_p(stream or None)))
+
+
+def bands_assembler(w: int, h: int, nranks: int, band_rows: int, slot_pixels: int):
+    """A callable (d_frame, d_slots, stream) -> None for rt_assemble_bands with its constant
+    arguments built once."""
+    fn = lib().rt_assemble_bands
+    a = (C.c_uint64(slot_pixels), C.c_uint32(w), C.c_uint32(h), C.c_int32(nranks), C.c_int32(band_rows))
+
+    def assemble(d_frame: int, d_slots: int, stream: int) -> None:
+        _stream_arg(stream)
+        rc = fn(d_frame, d_slots, *a, stream)
+        if rc:
+            _check(rc)
+    return assemble
 
 
 def assemble_bands(frame, chunks, w: int, h: int, band_rows: int):
