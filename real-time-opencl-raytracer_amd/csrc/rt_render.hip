@@ -218,6 +218,7 @@ struct rt_ctx {
     int2* d_leaf = nullptr;
     uint32_t root = 0;
     uint32_t n_inner = 0;
+    uint32_t rank_shift = 0;   // wavefront sort keys: leaf positions >> rank_shift fit 13 bits
     int fast_div = 0;
     int clean = 0;
     bool have_scene = false;
@@ -291,11 +292,11 @@ static int ensure(rt_ctx* c, T*& p, size_t& cap, size_t n) {
 // Per-bounce ray sort of the wavefront path (32-bit keys, 32-bit payloads).
 static hipError_t rtk_sort_temp_bytes(int n, size_t& bytes) {
     return hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, n);
+                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 16);
 }
 static hipError_t rtk_sort_pairs(uint8_t* tmp, size_t bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
                                  uint32_t* vout, int n, hipStream_t s) {
-    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, 32, s);
+    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, 16, s);
 }
 
 static void free_slot(rt_ctx::FrameSlot& f) {
@@ -638,6 +639,8 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
         c->root = ref_of[0];
         c->n_inner = (uint32_t)n_inner;
+        c->rank_shift = 0;
+        while (((uint64_t)std::max(nref, 1) >> c->rank_shift) > 0x1FFEu) ++c->rank_shift;
         c->fast_div = fast_ok ? 1 : 0;
         c->have_scene = true;
         ++c->scene_gen;
@@ -873,7 +876,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             if (sort) {
                 hipLaunchKernelGGL(rtk_strict::wf_key_kernel, dim3(1024), dim3(256), 0, s,
                                    (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, L.d_sort[0],
-                                   L.d_sort[1], c->d_rank);
+                                   L.d_sort[1], c->d_rank, c->rank_shift);
                 HIPC(c, rtk_sort_pairs(L.d_sort_tmp, L.sort_tmp_cap, L.d_sort[0], L.d_sort[2], L.d_sort[1],
                                        L.d_sort[3], (int)npix, s));
                 W.perm = L.d_sort[3];
