@@ -84,6 +84,9 @@
 #ifndef RTK_SCALAR_SHARE
 #define RTK_SCALAR_SHARE 0  // traverse_ifif: first active lane's record via the scalar cache for the lanes sharing it (A/B: slower)
 #endif
+#ifndef RTK_LANE_ROWS
+#define RTK_LANE_ROWS 0     // 1: row-major lanes in a tile; 0: Morton (2x2 pixel quads)
+#endif
 #ifndef RTK_TRI_PIPE
 #define RTK_TRI_PIPE 1      // fast traversal: next triangle record in flight while the current one is tested
 #endif
