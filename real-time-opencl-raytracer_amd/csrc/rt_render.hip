@@ -45,9 +45,6 @@
 #ifndef RTK_TRI_PREFETCH
 #define RTK_TRI_PREFETCH 0
 #endif
-#ifndef RTK_REFILL
-#define RTK_REFILL 16
-#endif
 #ifndef RTK_FUSED_WAVES
 #define RTK_FUSED_WAVES 4   // waves per block of the fused kernel: 1, 2 or 4
 #endif
