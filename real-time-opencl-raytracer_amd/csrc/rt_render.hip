@@ -21,8 +21,14 @@
 //    the rest spills to a per-pixel global region; the top of stack stays in a
 //    register.  Stack semantics (including the overflow -> miss rule at 65)
 //    are the reference's, entry for entry;
-//  * one wave = one 8x8 pixel tile (the reference's work-group), 4 waves per
-//    block, blocks remapped so each XCD's L2 sees a contiguous screen strip.
+//  * one wave = one 8x8 pixel tile (the reference's work-group, lanes in Morton
+//    order), 4 waves per block, blocks dispatched longest-first from the previous
+//    frame's per-tile times;
+//  * each lane takes one step of its own reference sequence per iteration (an
+//    inner visit or one triangle test: traverse_ifif), so a wave's length is its
+//    slowest ray, not the sum of its lanes' leaf rounds;
+//  * frame scratch is per stream, so frames enqueued on different streams run
+//    concurrently (frames in flight; multi-GPU band gather overlaps rendering).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
