@@ -5,6 +5,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 import rtamd
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,6 +39,13 @@ def test_abi_version_and_errors_without_gpu():
     assert lib.rt_abi_version() == 1
     assert lib.rt_set_params(None, None) == -1
     assert lib.rt_render(None, 1, 1, 1, 0, None, None) == -1
+    # rt_assemble_bands validates before any device call: null buffers, zero sizes, bad
+    # rank counts, and a slot too small for rank 0's bands are RT_ERR_INVALID_ARG
+    assert lib.rt_assemble_bands(None, None, 0, 0, 0, 0, 0, None) == -1
+    assert lib.rt_assemble_bands(16, 16, 100, 10, 10, 0, 8, None) == -1
+    assert lib.rt_assemble_bands(16, 16, 10, 10, 10, 2, 8, None) == -1   # rank 0 owns 8 rows = 80 px > 10
+    with pytest.raises(ValueError):   # the wrapper refuses torch's null stream
+        rtamd.assemble_bands_device(16, 16, 100, 10, 10, 1, 8, 0)
     assert rtamd.tiling_pixels(100, 50, 0, 1, 16) == 5000
     # bands of 16 rows over 50 rows, 3 ranks: rank 0 owns bands 0 and 3 (16 + 2 rows)
     assert rtamd.tiling_pixels(100, 50, 0, 3, 16) == 18 * 100
