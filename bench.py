@@ -91,6 +91,9 @@ def main():
     ap.add_argument("--band-rows", type=int, default=8,
                     help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
     ap.add_argument("--dist", action="store_true", help="use the process-group gather path even at N = 1")
+    ap.add_argument("--gather", default="native", choices=["torch", "native"],
+                    help="band exchange at N > 1: torch.distributed gather (async, RCCL) + rt_assemble_bands, or "
+                         "the library's own RCCL communicators on the frame's stream (rt_frame_gather)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="frames in flight (one stream each): frame i+1 renders while frame i drains / gathers")
     ap.add_argument("--shard", default="", help="R/N: render only rank R's bands of an N-way split (diagnostic)")
@@ -200,6 +203,40 @@ def main():
             frame_ptr = [f.data_ptr() for f in frames]
             gbuf_ptr = [g.data_ptr() for g in gbufs]
 
+    native = use_dist and args.gather == "native"
+    comms = []
+    if native:
+        # one communicator per in-flight stream; rank 0's ids travel through the process
+        # group's store.  If any rank cannot create them, every rank falls back to the
+        # torch.distributed gather (agreed through an all-reduce, so no rank is left waiting).
+        store = dist.distributed_c10d._get_default_store()
+        ok = 1.0
+        try:
+            for k in range(F):
+                key = f"rtamd_comm_{k}"
+                if rank == 0:   # an empty id tells every rank not to enter the collective init
+                    try:
+                        uid0 = rtamd.Comm.unique_id()
+                    except rtamd.RtError:
+                        uid0 = b""
+                    store.set(key, uid0)
+                uid = bytes(store.get(key))
+                if len(uid) != rtamd.Comm.ID_BYTES:
+                    raise rtamd.RtError(-2, "rank 0 has no RCCL id")
+                comms.append(rtamd.Comm(local, world, rank, uid))
+        except rtamd.RtError as e:
+            print(f"rank {rank}: native band exchange unavailable ({e}); using torch.distributed", file=sys.stderr)
+            ok = 0.0
+        flag = torch.tensor([ok], device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if flag.item() < 1.0:
+            native = False
+            for c in comms:
+                c.close()
+            comms = []
+        slots_ptr = [g.data_ptr() for g in gbufs] if rank == 0 else [0] * F
+        fr_ptr = [f.data_ptr() for f in frames] if rank == 0 else [0] * F
+
     def finish(k):
         work, pending[k] = pending[k], None
         work.wait()   # orders streams[k] (the current stream) after the gather
@@ -213,7 +250,9 @@ def main():
         if pending[k] is not None:
             finish(k)
         launch(out_ptr[k], sh[k])
-        if use_dist:   # dist.gather(outs[k], glists[k], dst=0, async_op=True) without its argument checks
+        if native:     # gather + assembly on the frame's own stream: no cross-stream waits
+            comms[k].frame_gather(out_ptr[k], cap, slots_ptr[k], fr_ptr[k], w, h, args.band_rows, sh[k])
+        elif use_dist:   # dist.gather(outs[k], glists[k], dst=0, async_op=True) without its argument checks
             pending[k] = pg.gather(g_out[k], g_in[k], gopts)
 
     def drain():
@@ -274,6 +313,8 @@ def main():
     if rank != 0:
         if world > 1:
             dist.barrier()
+            for c in comms:
+                c.close()
             dist.destroy_process_group()
         return
 
@@ -348,6 +389,8 @@ def main():
                    "primary_rays_per_frame": int(prim_total), "parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
                                    else f"shard {args.shard} of the band split (diagnostic, no gather)"),
                    "band_rows": args.band_rows, "frames_in_flight": F,
+                   "band_exchange": (None if not use_dist else "rt_frame_gather (library RCCL communicators)" if native
+                                     else "torch.distributed gather (RCCL) + rt_assemble_bands"),
                    "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                    "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4), "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)"
                                                         if args.bvh == "sbvh" else "binned SAH"),
@@ -370,6 +413,8 @@ def main():
     print(json.dumps(res))
     if use_dist:
         dist.barrier()
+        for c in comms:
+            c.close()
         dist.destroy_process_group()
 
 

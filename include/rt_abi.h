@@ -159,6 +159,22 @@ int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* tiling);
 int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint32_t w, uint32_t h,
                       int32_t nranks, int32_t band_rows, void* stream);
 
+/* Native band exchange for multi-GPU frames over RCCL: the reference
+ * reads the frame back to the host (RayTracer.cpp:343); here every rank's bands go to
+ * rank 0 on the frame's own stream.  One rt_comm per in-flight stream (a communicator's
+ * operations are serialised); the 128-byte id travels from rank 0 to the others over any
+ * channel (bench.py: the torch.distributed store). */
+typedef struct rt_comm rt_comm;
+int rt_comm_unique_id(uint8_t* id, int32_t id_bytes);
+int rt_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* id, int32_t id_bytes, rt_comm** out);
+int rt_comm_destroy(rt_comm* comm);
+const char* rt_comm_last_error(void);
+/* ncclGather of slot_pixels pixels from every rank's d_bands into rank 0's d_slots
+ * (nranks * slot_pixels), then on rank 0 rt_assemble_bands into d_frame; all on `stream`.
+ * Every rank calls it once per frame, in the same order. */
+int rt_frame_gather(rt_comm* comm, const uint32_t* d_bands, uint64_t slot_pixels, uint32_t* d_slots,
+                    uint32_t* d_frame, uint32_t w, uint32_t h, int32_t band_rows, void* stream);
+
 /* Kernel-side timing of the last render, from HIP events on the launch stream
  * (ms): total_ms = every kernel of the frame (counter reset / block-order
  * build, the first-bounce or fused render kernel, further bounces);

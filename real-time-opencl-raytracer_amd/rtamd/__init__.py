@@ -80,7 +80,8 @@ class rt_bvh_view(C.Structure):
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
 ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_device",
-               "rt_tiling_pixels", "rt_assemble_bands", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_tiling_pixels", "rt_assemble_bands", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
+               "rt_comm_last_error", "rt_frame_gather", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
@@ -115,6 +116,11 @@ def lib() -> C.CDLL:
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
             "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
             "rt_assemble_bands": (C.c_int, [vp, vp, C.c_uint64, u32, u32, i32, i32, vp]),
+            "rt_comm_unique_id": (C.c_int, [vp, i32]),
+            "rt_comm_create": (C.c_int, [i32, i32, i32, vp, i32, C.POINTER(vp)]),
+            "rt_comm_destroy": (C.c_int, [vp]),
+            "rt_comm_last_error": (C.c_char_p, []),
+            "rt_frame_gather": (C.c_int, [vp, vp, C.c_uint64, vp, vp, u32, u32, i32, vp]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
             "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
             "rt_last_deferred": (C.c_int, [vp, C.POINTER(u32)]),
@@ -488,6 +494,45 @@ def rank_bands(h: int, rank: int, nranks: int, band_rows: int):
     (band b belongs to rank b % nranks; same rule as rt_tiling in include/rt_abi.h)."""
     nbands = (h + band_rows - 1) // band_rows
     return [(b * band_rows, min(band_rows, h - b * band_rows)) for b in range(rank, nbands, nranks)]
+
+
+class Comm:
+    """One RCCL communicator for the native band exchange (rt_comm_*, include/rt_abi.h):
+    rank 0 makes the 128-byte id (Comm.unique_id()), every rank passes it to Comm(...)."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * Comm.ID_BYTES)()
+        rc = lib().rt_comm_unique_id(buf, Comm.ID_BYTES)
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+        return bytes(buf)
+
+    def __init__(self, device: int, nranks: int, rank: int, uid: bytes):
+        buf = (C.c_uint8 * Comm.ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        rc = lib().rt_comm_create(device, nranks, rank, buf, Comm.ID_BYTES, C.byref(h))
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+        self._h, self.rank, self.nranks = h, rank, nranks
+        self._fn = lib().rt_frame_gather
+
+    def frame_gather(self, d_bands: int, slot_pixels: int, d_slots: int, d_frame: int, w: int, h: int,
+                     band_rows: int, stream: int) -> None:
+        """rt_frame_gather: every rank's bands to rank 0's slots, then rank 0 assembles the frame."""
+        _stream_arg(stream)
+        rc = self._fn(self._h, d_bands, slot_pixels, d_slots or None, d_frame or None, w, h, band_rows, stream)
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rt_comm_destroy(self._h)
+            self._h = None
+
+    __del__ = close
 
 
 def _stream_arg(stream):
