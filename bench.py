@@ -85,8 +85,8 @@ def make_scene(cfg, threads, builder="sbvh", via_dae=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=500)   # 0.2 s of frames: steady state, not clock ramp-up
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--band-rows", type=int, default=8,
                     help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
