@@ -96,6 +96,20 @@
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
 #endif
+// Quad-synchronised if-if steps: inner and triangle records are laid out
+// at their position in the BVH's left-first depth-first order (one index space, both
+// arrays sparse), so a ref IS its DFS key; in each quad of lanes only the lanes whose next
+// step comes first in that order step (a lane that waited RTK_QS_WAIT iterations steps
+// anyway), so lanes that will fetch the same record do it in the same iteration.
+#ifndef RTK_QUAD_SYNC
+#define RTK_QUAD_SYNC 0
+#endif
+#ifndef RTK_QS_WAIT
+#define RTK_QS_WAIT 8
+#endif
+#if RTK_QUAD_SYNC && RTK_NODE_CACHE
+#error "RTK_NODE_CACHE needs the BFS-top inner numbering; RTK_QUAD_SYNC uses DFS positions"
+#endif
 
 namespace rtk {
 
@@ -109,8 +123,8 @@ constexpr int kLdsStack = RTK_LDS_STACK;
 constexpr int kGlobalStack = 64 - kLdsStack;         // slots kLdsStack..63
 
 struct DevScene {
-    const float4* __restrict__ wnodes;   // [n_inner][4]
-    const float4* __restrict__ tris;     // [n_refs][3]
+    const float4* __restrict__ wnodes;   // [n_inner][4] (RTK_QUAD_SYNC: [DFS positions][4], sparse)
+    const float4* __restrict__ tris;     // [n_refs][3]  (RTK_QUAD_SYNC: [DFS positions][3], sparse)
     const float4* __restrict__ shade;    // [n_tris][7]
     const int2* __restrict__ leaf_table; // escape leaves {offset, count}
     uint32_t root;
@@ -500,6 +514,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
     std::vector<int32_t> inner_id(nn, -1);
     std::vector<int2> leaf_table;
     std::vector<uint32_t> ref_of(nn, 0);
+    std::vector<int64_t> leaf_pos(nn, -1);   // RTK_QUAD_SYNC: a reachable leaf's first triangle record
     // inner ids in pre-order of reachability from the root; detect cycles (the
     // reference would spin forever on some of them).
     {
@@ -529,9 +544,37 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             state[n] = 2;
             stk.pop_back();
         }
-        // Renumber: the first kBfsTop inner nodes in breadth-first order from the root get
-        // ids 0..kBfsTop-1 (the top of the tree, which every ray walks: the fast kernel keeps
-        // the first RTK_NODE_CACHE of them in LDS); the rest keep their pre-order.
+        // RTK_QUAD_SYNC: inner records and the triangle records of each reachable leaf take
+        // their position in the left-first depth-first order of the reachable tree (one
+        // index space for both arrays), so a ref is its own DFS key (rt_kernel_body.inc
+        // traverse_ifif).  Otherwise: the first kBfsTop inner nodes in breadth-first order
+        // from the root get ids 0..kBfsTop-1 (the top of the tree, which every ray walks:
+        // the fast kernel keeps the first RTK_NODE_CACHE of them in LDS); the rest keep
+        // their pre-order.
+#if RTK_QUAD_SYNC
+        {
+            std::vector<int32_t> dfs{0};
+            std::vector<uint8_t> seen(nn, 0);
+            int64_t pos = 0;
+            while (!dfs.empty()) {
+                const int32_t n = dfs.back();
+                dfs.pop_back();
+                if (seen[n]) continue;
+                seen[n] = 1;
+                const rt_bvh_node& nd = nodes[n];
+                if (inner_id[n] >= 0) {
+                    inner_id[n] = (int32_t)pos++;
+                    dfs.push_back(nd.offset_right);
+                    dfs.push_back(nd.offset_left);
+                } else if (nd.offset_left < 0) {
+                    leaf_pos[n] = pos;
+                    pos += nd.num_tris < 0 ? 0 : nd.num_tris;
+                }
+                if (pos >= (int64_t)1 << 30) return set_err(c, "BVH too large for the DFS layout", RT_ERR_BAD_SCENE);
+            }
+            next = (int32_t)pos;
+        }
+#else
         {
             constexpr int32_t kBfsTop = 1024;
             std::vector<int32_t> bfs;
@@ -553,6 +596,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             for (int32_t o = 0; o < next; ++o)
                 if (!seen[by_old[o]]) inner_id[by_old[o]] = id++;
         }
+#endif
         bool clean = true;
         for (int32_t n = 0; n < nn; ++n)
             if (state[n] != 0 && nodes[n].offset_left >= 0 && inner_id[n] < 0) clean = false;
@@ -566,6 +610,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
                 if (cnt > 0 && (off < 0 || (int64_t)off + cnt > nref))
                     return set_err(c, "leaf triangle range out of bounds", RT_ERR_BAD_SCENE);
                 if (cnt == 0) off = 0;
+                if (RTK_QUAD_SYNC) off = leaf_pos[n] < 0 ? 0 : (int32_t)leaf_pos[n];
                 if (cnt < (int32_t)rtk::kCntEscape && off < (1 << 26)) {
                     ref_of[n] = rtk::kLeafBit | ((uint32_t)cnt << 26) | (uint32_t)off;
                 } else {
@@ -602,15 +647,23 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         }
         // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974)
         // + a 16-B tail pad: traverse_ifif fetches 64 B at a triangle record (48 B used)
-        std::vector<float4> tr((size_t)std::max(nref, 1) * 3 + 1, make_float4(0, 0, 0, 0));
-        for (int32_t i = 0; i < nref; ++i) {
-            const int32_t tri1 = refs[i];
+        // (RTK_QUAD_SYNC: each reachable leaf's references copied to its DFS positions)
+        const int32_t ntrec = RTK_QUAD_SYNC ? n_inner : nref;
+        std::vector<float4> tr((size_t)std::max(ntrec, 1) * 3 + 1, make_float4(0, 0, 0, 0));
+        auto put_tri = [&](int64_t at, int32_t tri1) {
             const rt_float4 v0 = verts[idx[tri1]], v1 = verts[idx[tri1 + 1]], v2 = verts[idx[tri1 + 2]];
             float idf;
             std::memcpy(&idf, &tri1, 4);
-            tr[(size_t)i * 3 + 0] = make_float4(v0.x, v0.y, v0.z, idf);
-            tr[(size_t)i * 3 + 1] = make_float4(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z, 0.0f);
-            tr[(size_t)i * 3 + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.0f);
+            tr[(size_t)at * 3 + 0] = make_float4(v0.x, v0.y, v0.z, idf);
+            tr[(size_t)at * 3 + 1] = make_float4(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z, 0.0f);
+            tr[(size_t)at * 3 + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.0f);
+        };
+        if (RTK_QUAD_SYNC) {
+            for (int32_t n = 0; n < nn; ++n)
+                if (leaf_pos[n] >= 0)
+                    for (int32_t i = 0; i < nodes[n].num_tris; ++i) put_tri(leaf_pos[n] + i, refs[nodes[n].offset_tris + i]);
+        } else {
+            for (int32_t i = 0; i < nref; ++i) put_tri(i, refs[i]);
         }
         // per-triangle shading records (volumeRender.cl:1306-1374)
         std::vector<float4> sh((size_t)ntri * 7);
