@@ -293,6 +293,25 @@ def main():
     # records on the launch stream around each frame's kernels (ring of 64 frames)
     frame_ms_avg, kernel_ms_avg = r.timing_average(min(args.steps, 64))
 
+    # (untimed for `value`) the reference's own boundary: rt_render, synchronous, the frame
+    # read back into host memory (raytrace_gpgpu: launch + clFinish + clEnqueueReadBuffer,
+    # RayTracer.cpp:330-344); pageable numpy and pinned host buffers
+    host_boundary = None
+    if world == 1 and not args.shard:
+        def host_rate(buf_ptr, n=20):
+            r.render_host_ptr(w, h, depth, flags, buf_ptr)
+            t1 = time.perf_counter()
+            for _ in range(n):
+                r.render_host_ptr(w, h, depth, flags, buf_ptr)
+            return (time.perf_counter() - t1) / n * 1e3
+        pageable = np.zeros(w * h, np.uint32)
+        pinned = torch.zeros(w * h, dtype=torch.int32, pin_memory=True)
+        ms_pg = host_rate(pageable.ctypes.data)
+        ms_pin = host_rate(pinned.data_ptr())
+        host_boundary = {"api": "rt_render (synchronous, frame copied to host memory)",
+                         "ms_per_frame_pageable": round(ms_pg, 4), "ms_per_frame_pinned": round(ms_pin, 4),
+                         "mrays_per_s_pinned": round(rays_local / (ms_pin * 1e-3) / 1e6, 1)}
+
     if use_dist:
         t = torch.tensor([elapsed, float(rays_local), float(prim_local)], dtype=torch.float64, device=dev)
         tmax = t[:1].clone()
@@ -410,6 +429,8 @@ def main():
     }
     if frame_ok is not None:
         res["config"]["gathered_frame_equals_single_rank_render"] = frame_ok
+    if host_boundary is not None:
+        res["config"]["host_boundary"] = host_boundary
     print(json.dumps(res))
     if use_dist:
         dist.barrier()

@@ -430,6 +430,12 @@ class Renderer:
         _check(lib().rt_render(self._h, w, h, depth, flags, _ptr(out), None), self._h)
         return out
 
+    def render_host_ptr(self, w: int, h: int, depth: int, flags: int, host_ptr: int) -> None:
+        """rt_render into caller-owned host memory at `host_ptr` (w*h uint32, pageable or pinned)."""
+        if not host_ptr:
+            raise ValueError("render_host_ptr: null output pointer")
+        _check(lib().rt_render(self._h, w, h, depth, flags, C.c_void_p(host_ptr), None), self._h)
+
     def render_device(self, w, h, depth, flags, d_out_ptr: int, tiling: Optional[rt_tiling] = None,
                       stream: Optional[int] = None, aux_ptrs=None):
         """Enqueue a frame on `stream` (a hipStream_t handle, e.g. torch.cuda.Stream().cuda_stream);

@@ -72,6 +72,24 @@ def test_odd_sizes(renderer):
         _compare(gpu, _oracle(d, 3, w=w, h=h, params=p), f"{w}x{h}")
 
 
+def test_render_into_pinned_and_pageable_host_memory(renderer):
+    """rt_render's frame read-back lands the same pixels in pinned and pageable host memory."""
+    import torch
+    d = load_golden("knot16k")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    ref = _oracle(d, 1)["out"]
+    pageable = np.zeros(w * h, np.uint32)
+    renderer.render_host_ptr(w, h, 1, 0, pageable.ctypes.data)
+    pinned = torch.zeros(w * h, dtype=torch.int32, pin_memory=True)
+    renderer.render_host_ptr(w, h, 1, 0, pinned.data_ptr())
+    assert np.array_equal(pageable, ref)
+    assert np.array_equal(pinned.numpy().view(np.uint32), ref)
+    with pytest.raises(ValueError):
+        renderer.render_host_ptr(w, h, 1, 0, 0)
+
+
 def test_overflow_counter(renderer):
     d = load_golden("overflow_comb")
     renderer.upload(_scene(d))
