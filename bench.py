@@ -47,12 +47,19 @@ CONFIGS = {
     # configs[3]: C3 scene at 4K (multi-GPU scaling curve)
     "c4": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=HF_EXT, w=3840, h=2160, depth=1, flags=0,
                desc="C4: C3 scene at 3840x2160, primary + 1 shadow ray"),
-    # configs[4]: 10M tris (10 x C3 on a 5x2 grid), depth 3 (primary + 2 bounces, shadows)
-    # flags 8 = RT_FLAG_WAVEFRONT: with frames in flight the per-bounce launches beat the fused
-    # kernel (5.4 vs 4.9 Grays/s; one frame at a time the fused kernel wins)
-    "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920, h=1080, depth=3, flags=8,
+    # configs[4]: 10M tris (10 x C3 on a 5x2 grid), depth 3 (primary + 2 bounces, shadows), in
+    # the wavefront mode with per-bounce ray sorting, as the config names it: flags 8 | 32 =
+    # RT_FLAG_WAVEFRONT | RT_FLAG_WF_SORT
+    "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920, h=1080, depth=3,
+               flags=8 | 32,
                dae=False,  # a 1 GB Collada text file is not worth the round trip; built in memory
-               desc="C5: 10M-tri merged scene (10 x C3 on a 5x2 grid), 1920x1080, 3 bounces with shadows"),
+               desc="C5: 10M-tri merged scene (10 x C3 on a 5x2 grid), 1920x1080, 3 bounces with shadows, "
+                    "wavefront mode with per-bounce ray sorting"),
+    # the same without the sort: faster here, the sort costs more than the coherence it buys;
+    # with frames in flight the per-bounce launches also beat the fused kernel
+    "c5u": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920, h=1080, depth=3,
+                flags=8, dae=False,
+                desc="C5 scene and frame, wavefront mode without ray sorting"),
 }
 
 
@@ -372,6 +379,20 @@ def main():
                "sample": f"oracle/rt_oracle.c on every {stride}th pixel of the same frame ({npix_sample} px, "
                          f"{cpu_rays} rays) x {reps} repetition(s), {cpu_s:.1f} s, {ncores} threads"}
 
+    # measured device copy rate (the roofline also against a measured stream-copy
+    # peak): 1 GiB -> 1 GiB device-to-device copies, read + write bytes over HIP-event time
+    src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(10):
+        dst.copy_(src)
+    ev1.record()
+    ev1.synchronize()
+    stream_copy_gbs = 10 * 2 * src.numel() * 4 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
+    del src, dst
+
     # algorithmic bytes per launch = rays this launch traces x bytes/ray + 4 B/pixel output
     launch_rays = rays_total / max(1, world)
     launch_px = (w * h) / world if world > 1 else npx
@@ -405,7 +426,9 @@ def main():
         "config": {"workload": cfg["desc"], "config": args.config, "triangles": mesh.num_triangles,
                    "bvh_nodes": int(bvh.nodes.shape[0]), "width": w, "height": h, "depth": depth,
                    "shadow": not (flags & 1), "rays_per_frame": int(rays_total),
-                   "primary_rays_per_frame": int(prim_total), "parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
+                   "primary_rays_per_frame": int(prim_total),
+                   "primary_mrays_per_s": round(prim_total * args.steps / elapsed / 1e6, 1),
+                   "mpixels_per_s": round(w * h * args.steps / elapsed / 1e6, 1),"parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
                                    else f"shard {args.shard} of the band split (diagnostic, no gather)"),
                    "band_rows": args.band_rows, "frames_in_flight": F,
                    "band_exchange": (None if not use_dist else "rt_frame_gather (library RCCL communicators)" if native
@@ -420,6 +443,8 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "achieved_aggregate": round(achieved_aggregate, 2),
                      "frac_aggregate": round(achieved_aggregate / HBM_PEAK_GBS, 4),
+                     "stream_copy_gbs": round(stream_copy_gbs, 1),
+                     "frac_of_stream_copy": round(achieved / stream_copy_gbs, 4),
                      "launches_overlap": F > 1,
                      "bytes_per_ray": round(bpr, 1), "kernel_ms": round(kernel_ms_avg, 4),
                      "frame_kernels_ms": round(frame_ms_avg, 4),
