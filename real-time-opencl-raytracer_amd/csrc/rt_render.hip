@@ -96,6 +96,12 @@
 #ifndef RTK_XCD_CHUNK
 #define RTK_XCD_CHUNK 4
 #endif
+#ifndef RTK_SORT_BITS
+#define RTK_SORT_BITS 8     // wavefront ray-sort key width: 8 = one radix pass, 16 = two (A/B)
+#endif
+#if RTK_SORT_BITS < 4 || RTK_SORT_BITS > 16
+#error "RTK_SORT_BITS must be in 4..16"
+#endif
 // Quad-synchronised if-if steps: inner and triangle records are laid out
 // at their position in the BVH's left-first depth-first order (one index space, both
 // arrays sparse), so a ref IS its DFS key; in each quad of lanes only the lanes whose next
@@ -309,14 +315,14 @@ static int ensure(rt_ctx* c, T*& p, size_t& cap, size_t n) {
     return RT_OK;
 }
 
-// Per-bounce ray sort of the wavefront path (32-bit keys, 32-bit payloads).
+// Per-bounce ray sort of the wavefront path (RTK_SORT_BITS of 32-bit keys, 32-bit payloads).
 static hipError_t rtk_sort_temp_bytes(int n, size_t& bytes) {
     return hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 16);
+                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, RTK_SORT_BITS);
 }
 static hipError_t rtk_sort_pairs(uint8_t* tmp, size_t bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
                                  uint32_t* vout, int n, hipStream_t s) {
-    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, 16, s);
+    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, RTK_SORT_BITS, s);
 }
 
 static void free_slot(rt_ctx::FrameSlot& f) {
