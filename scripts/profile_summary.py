@@ -36,6 +36,20 @@ def main():
     for r in csv.DictReader(open(stats)):
         if KERNEL in r["Name"]:
             avg_ns = float(r["AverageNs"])
+    # the traced run's timed window: launch order is 1 aux-count render, W warm-up frames,
+    # K timed frames, then bench.py's host-boundary renders; compare with the HIP-event
+    # average bench.py printed for the same K frames
+    timed_us = hip_ms = None
+    trace = glob.glob(os.path.join(ROOT, "gpurun_out", "prof_trace", "**", "*kernel_trace.csv"), recursive=True)
+    tlog = os.path.join(ROOT, "gpurun_out", "prof_trace.log")
+    if trace and os.path.exists(tlog):
+        j = json.loads([ln for ln in open(tlog) if ln.startswith("{")][-1])
+        rows = sorted((r for r in csv.DictReader(open(trace[0])) if KERNEL in r["Kernel_Name"]),
+                      key=lambda r: int(r["Start_Timestamp"]))
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+        t = d[1 + j["warmup"]: 1 + j["warmup"] + j["steps"]]
+        timed_us = round(sum(t) / len(t), 2) if t else None
+        hip_ms = j["roofline"]["kernel_ms"]
     fetch, nf, ff = counter("prof_fetch", "FETCH_SIZE")
     write, nw, fw = counter("prof_write", "WRITE_SIZE")
     shutil.copy(ff, os.path.join(out, f"{cfg}_pmc_fetch.csv"))
@@ -47,6 +61,10 @@ def main():
     res = {
         "config": cfg, "kernel": "rtk_strict::" + KERNEL, "round": rnd,
         "rocprof_avg_kernel_us": None if avg_ns is None else round(avg_ns / 1e3, 2),
+        "rocprof_avg_timed_window_us": timed_us,
+        "hip_event_avg_timed_window_ms": hip_ms,
+        "note": "rocprof_avg_kernel_us averages every launch of the traced run (warm-up, timed frames, and the "
+                "one-at-a-time host-boundary renders); the timed-window average is the one bench.py reports",
         "FETCH_SIZE_kB_median": fetch, "WRITE_SIZE_kB_median": write, "dispatches": [nf, nw],
         "correction": "FETCH_SIZE x2 (gfx950 reports half the bytes of 16B/lane reads, MI355X_MICROARCH.md HBM); "
                       "kB = 1024 B",
