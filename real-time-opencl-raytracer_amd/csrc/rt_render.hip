@@ -102,6 +102,12 @@
 #if RTK_SORT_BITS < 4 || RTK_SORT_BITS > 16
 #error "RTK_SORT_BITS must be in 4..16"
 #endif
+#ifndef RTK_COUNT_SORT
+#define RTK_COUNT_SORT 1    // wavefront ray sort: 256-bucket counting sort over the live queue (0: hipCUB radix sort)
+#endif
+#if RTK_COUNT_SORT && RTK_SORT_BITS != 8
+#error "RTK_COUNT_SORT sorts 8-bit keys"
+#endif
 // Quad-synchronised if-if steps: inner and triangle records are laid out
 // at their position in the BVH's left-first depth-first order (one index space, both
 // arrays sparse), so a ref IS its DFS key; in each quad of lanes only the lanes whose next
@@ -289,9 +295,11 @@ struct rt_ctx {
 
 static std::string g_err;
 
-// frame counter buffer (d_wcnt): 8 per bounce, then the restart count
+// frame counter buffer (d_wcnt): 8 per bounce, then the restart count, then per bounce
+// the counting sort's bucket histogram and cursors (256 + 256)
 constexpr size_t kRestartSlot = 8 * (RT_MAX_DEPTH + 1);
-constexpr size_t kCounters = kRestartSlot + 1;
+constexpr size_t kSortSlot = kRestartSlot + 1;
+constexpr size_t kCounters = kSortSlot + 512 * RT_MAX_DEPTH;
 
 static int set_err(rt_ctx* c, const std::string& m, int code) {
     if (c) c->err = m; else g_err = m;
@@ -944,7 +952,16 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.in = qbuf(k);
             W.in_count = cnt + 8 * k + 0;
             W.perm = nullptr;
-            if (sort) {
+            if (sort && RTK_COUNT_SORT) {
+                uint32_t* hist = cnt + kSortSlot + 512 * (size_t)k;   // zeroed with the frame's counters
+                hipLaunchKernelGGL(rtk_strict::wf_hist_kernel, dim3(1024), dim3(256), 0, s, (const rtk::QRay*)qbuf(k),
+                                   (const uint32_t*)(cnt + 8 * k + 0), (const uint32_t*)c->d_rank, c->rank_shift,
+                                   (uint8_t*)L.d_sort[0], hist);
+                hipLaunchKernelGGL(rtk_strict::wf_scatter_kernel, dim3(1024), dim3(256), 0, s,
+                                   (const uint32_t*)(cnt + 8 * k + 0), (const uint8_t*)L.d_sort[0],
+                                   (const uint32_t*)hist, hist + 256, L.d_sort[3]);
+                W.perm = L.d_sort[3];
+            } else if (sort) {
                 hipLaunchKernelGGL(rtk_strict::wf_key_kernel, dim3(1024), dim3(256), 0, s,
                                    (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, L.d_sort[0],
                                    L.d_sort[1], c->d_rank, c->rank_shift);
