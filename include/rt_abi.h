@@ -64,25 +64,33 @@ enum {
     RT_ERR_BAD_SCENE = -5    /* index out of range in the uploaded arrays */
 };
 
-/* rt_render flags */
+/* rt_render flags.
+ * Arithmetic.  Without a math flag the kernel computes S_ref: the
+ * reference kernel exactly as the reference host builds it (RayTracer.cpp:2173,
+ * clBuildProgram with no options: OpenCL-default contraction, 2.5-ulp `/`, 3-ulp
+ * sqrt, the device library's rsqrt/pow) -- the same pixels as the reference on
+ * gfx950.  The two flags below select the alternatives. */
 enum {
     RT_FLAG_NO_SHADOW = 1u,  /* config C2 "primary rays only": skip the any-hit shadow ray
                                 (volumeRender.cl:1437-1460); coefficient stays 1 */
-    RT_FLAG_HW_MATH = 2u,    /* S_hw arithmetic: normalize's rsqrt and GGX's pow use the gfx950
-                                device-library functions the reference kernel links
-                                (v_rsq_f32, __ocml_pow_f32) instead of the S_strict
-                                CPU-reproducible ones */
+    RT_FLAG_HW_MATH = 2u,    /* S_hw arithmetic: the reference built with
+                                -cl-fp32-correctly-rounded-divide-sqrt -ffp-contract=off
+                                (IEEE `/` and sqrt, no contraction, the device library's
+                                rsqrt/pow: v_rsq_f32, __ocml_pow_f32) */
+    RT_FLAG_STRICT_MATH = 64u, /* S_strict arithmetic: S_hw with rsqrt and pow(x,5) computed in
+                                binary64 and rounded, reproducible on any IEEE host: the CPU
+                                oracle's arithmetic (oracle/rt_oracle.c).  Excludes RT_FLAG_HW_MATH. */
     RT_FLAG_WAVEFRONT = 8u,  /* wavefront mode: bounce 0 over screen tiles, then one
                                 launch per further bounce over a compacted queue of the rays still in
                                 flight, instead of the fused one-lane-per-pixel kernel; bit-identical.
                                 Depth-1 frames always run as that first launch alone. */
     RT_FLAG_WF_SORT = 32u,   /* with RT_FLAG_WAVEFRONT: sort each bounce's queue by (direction octant,
                                 leaf position of the triangle the ray leaves) before tracing it */
-    RT_FLAG_EXACT_DIV = 4u,  /* force the IEEE-division slab test (volumeRender.cl:614-615) instead of
-                                the bit-identical 3-op fast quotient; for A/B only */
-    RT_FLAG_STATIC_ORDER = 16u /* fused kernel: keep the static XCD-dealt block order instead of the
-                                adaptive longest-first order built from the previous frame's per-tile
-                                times; pixels are identical either way */
+    RT_FLAG_EXACT_DIV = 4u,  /* force the division form of the slab test (volumeRender.cl:614-615) instead
+                                of the bit-identical fast quotient; for A/B only */
+    RT_FLAG_STATIC_ORDER = 16u /* keep the static XCD-dealt block order instead of the adaptive
+                                longest-first order built from the previous frame's per-block times
+                                (DESIGN.md 6.2); pixels are identical either way */
 };
 
 #define RT_MAX_DEPTH 8       /* reference: RAY_TRACE_DEPTH 3 (volumeRender.cl:12) */

@@ -2,8 +2,9 @@
 //
 // Replaces the reference's per-pixel OpenCL kernel raytracer_bvh
 // (x64/Release/volumeRender.cl:1043-1547) and its host glue (RayTracer.cpp).
-// Results follow the reference kernel's arithmetic exactly; what
-// changes is how the data sits in HBM and how the traversal is scheduled:
+// Results follow the reference kernel's arithmetic exactly (S_ref,
+// the reference as its host builds it, by default; S_strict and S_hw by flag);
+// what changes is how the data sits in HBM and how the traversal is scheduled:
 //
 //  * inner BVH nodes are re-laid out as 64-B records that carry BOTH child
 //    boxes plus the two child references (one 64-B fetch per inner visit
@@ -22,11 +23,11 @@
 //    register.  Stack semantics (including the overflow -> miss rule at 65)
 //    are the reference's, entry for entry;
 //  * one wave = one 8x8 pixel tile (the reference's work-group, lanes in Morton
-//    order), 4 waves per block, blocks dispatched longest-first from the previous
-//    frame's per-tile times;
-//  * each lane takes one step of its own reference sequence per iteration (an
-//    inner visit or one triangle test: traverse_ifif), so a wave's length is its
-//    slowest ray, not the sum of its lanes' leaf rounds;
+//    order), 4 waves per block; each lane takes one step of its own reference
+//    sequence per iteration (traverse_ifif), so a wave's length is its slowest
+//    ray, not the sum of its lanes' leaf rounds;
+//  * blocks run longest-first, ordered by the previous frame's per-block times;
+//    the frame's last-finishing block builds that order in-kernel (no extra launch);
 //  * frame scratch is per stream, so frames enqueued on different streams run
 //    concurrently (frames in flight; multi-GPU band gather overlaps rendering).
 #include <hip/hip_runtime.h>
@@ -40,87 +41,9 @@
 #include <vector>
 
 #include "rt_abi.h"
-#include <hipcub/hipcub.hpp>
 
 #ifndef RTK_LDS_STACK
-#define RTK_LDS_STACK 20
-#endif
-#ifndef RTK_WHILE_WHILE
-#define RTK_WHILE_WHILE 1
-#endif
-#ifndef RTK_TRI_PREFETCH
-#define RTK_TRI_PREFETCH 0
-#endif
-#ifndef RTK_FUSED_WAVES
-#define RTK_FUSED_WAVES 4   // waves per block of the fused kernel: 1, 2 or 4
-#endif
-#ifndef RTK_MIN_WAVES
-#define RTK_MIN_WAVES 7     // __launch_bounds__ minimum waves per SIMD (fused kernel)
-#endif
-#ifndef RTK_MULTI_MIN_WAVES
-#define RTK_MULTI_MIN_WAVES 7   // render_kernel / wf_bounce_kernel (multi-bounce state)
-#endif
-#ifndef RTK_TILE_ORDER
-#define RTK_TILE_ORDER 1   // fused-kernel tile order policy (tile_order_table), env RTAMD_TILE_ORDER
-#endif
-#ifndef RTK_SCALAR_NODES
-#define RTK_SCALAR_NODES 0  // wave-uniform node / leaf fetches through the scalar cache (A/B: slower)
-#endif
-#ifndef RTK_WAVE_TIMES
-#define RTK_WAVE_TIMES 0    // diagnostic build: per-pixel start/end timestamps (env RTAMD_WAVE_TIMES=file)
-#endif
-#ifndef RTK_PROBE_VALU
-#define RTK_PROBE_VALU 0
-#endif
-#ifndef RTK_PROBE_EXTRA_LOAD
-#define RTK_PROBE_EXTRA_LOAD 0
-#endif
-#ifndef RTK_PERSISTENT
-#define RTK_PERSISTENT 0   // first_bounce_kernel: persistent waves over a tile counter (A/B: slower)
-#endif
-#ifndef RTK_IFIF
-#define RTK_IFIF 1          // fast traversal: lane-independent steps (traverse_ifif) instead of while-while
-#endif
-#ifndef RTK_NODE_CACHE
-#define RTK_NODE_CACHE 0    // depth-1 fast kernel: inner records (BFS top) copied into each block's LDS (A/B: slower)
-#endif
-#ifndef RTK_SCALAR_SHARE
-#define RTK_SCALAR_SHARE 0  // traverse_ifif: first active lane's record via the scalar cache for the lanes sharing it (A/B: slower)
-#endif
-#ifndef RTK_LANE_ROWS
-#define RTK_LANE_ROWS 0     // 1: row-major lanes in a tile; 0: Morton (2x2 pixel quads)
-#endif
-#ifndef RTK_TRI_PIPE
-#define RTK_TRI_PIPE 1      // fast traversal: next triangle record in flight while the current one is tested
-#endif
-#ifndef RTK_XCD_CHUNK
-#define RTK_XCD_CHUNK 4
-#endif
-#ifndef RTK_SORT_BITS
-#define RTK_SORT_BITS 8     // wavefront ray-sort key width: 8 = one radix pass, 16 = two (A/B)
-#endif
-#if RTK_SORT_BITS < 4 || RTK_SORT_BITS > 16
-#error "RTK_SORT_BITS must be in 4..16"
-#endif
-#ifndef RTK_COUNT_SORT
-#define RTK_COUNT_SORT 1    // wavefront ray sort: 256-bucket counting sort over the live queue (0: hipCUB radix sort)
-#endif
-#if RTK_COUNT_SORT && RTK_SORT_BITS != 8
-#error "RTK_COUNT_SORT sorts 8-bit keys"
-#endif
-// Quad-synchronised if-if steps: inner and triangle records are laid out
-// at their position in the BVH's left-first depth-first order (one index space, both
-// arrays sparse), so a ref IS its DFS key; in each quad of lanes only the lanes whose next
-// step comes first in that order step (a lane that waited RTK_QS_WAIT iterations steps
-// anyway), so lanes that will fetch the same record do it in the same iteration.
-#ifndef RTK_QUAD_SYNC
-#define RTK_QUAD_SYNC 0
-#endif
-#ifndef RTK_QS_WAIT
-#define RTK_QS_WAIT 8
-#endif
-#if RTK_QUAD_SYNC && RTK_NODE_CACHE
-#error "RTK_NODE_CACHE needs the BFS-top inner numbering; RTK_QUAD_SYNC uses DFS positions"
+#define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
 #endif
 
 namespace rtk {
@@ -130,13 +53,13 @@ constexpr float kTmin = 0.001f;                      // volumeRender.cl:640
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kRefError = 0x7FFFFFFFu;          // popped -> traversal returns -1
 constexpr uint32_t kCntEscape = 31u;
-constexpr int kWavesPerBlock = 4;
 constexpr int kLdsStack = RTK_LDS_STACK;
 constexpr int kGlobalStack = 64 - kLdsStack;         // slots kLdsStack..63
+constexpr uint32_t kBlockPx = 16;                    // a block = 2 x 2 tiles of 8 x 8 pixels
 
 struct DevScene {
-    const float4* __restrict__ wnodes;   // [n_inner][4] (RTK_QUAD_SYNC: [DFS positions][4], sparse)
-    const float4* __restrict__ tris;     // [n_refs][3]  (RTK_QUAD_SYNC: [DFS positions][3], sparse)
+    const float4* __restrict__ wnodes;   // [n_inner][4]
+    const float4* __restrict__ tris;     // [n_refs][3]
     const float4* __restrict__ shade;    // [n_tris][7]
     const int2* __restrict__ leaf_table; // escape leaves {offset, count}
     uint32_t root;
@@ -152,24 +75,24 @@ struct Frame {
     uint32_t flags;
     int32_t rank, nranks, band_rows;
     uint32_t local_rows;
-    uint32_t tiles_x, tiles_y, num_blocks;
-    const uint32_t* tile_order;   // [num_blocks] block -> tile, or null (in-kernel chunk dealing)
-    uint32_t* tile_cost;          // [num_blocks] per-tile wall time of this frame (adaptive order), or null
-    // persistent first-bounce kernel: 8x8 tiles taken from a counter (null = one block per tile group)
-    uint32_t* work_counter;
-    uint32_t tiles8_x, num_tiles8;
+    uint32_t tiles_x, tiles_y, num_blocks;   // blocks of kBlockPx x kBlockPx pixels
+    const uint32_t* tile_order;   // [num_blocks] block -> tile (static column strips, or longest-first)
+    uint32_t* tile_cost;          // [num_blocks] per-tile time of this frame (adaptive order), or null
+    uint32_t* lpt_next;           // [num_blocks] longest-first order for the next frame on this slot
+    uint32_t* done;               // blocks finished so far (the last one builds lpt_next)
+    uint32_t* zero_next;          // the other parity's frame counters, zeroed by this frame
+    uint32_t nzero;
 };
 
-// Wavefront path (rt_kernel_body.inc): a ray in flight between bounces --
-// {pix, o.xyz}, {d.xyz, shadow_sum}, {colour.xyz, 3 * triangle it leaves from}.
+// A ray in flight between bounces: {pix, o.xyz}, {d.xyz, shadow_sum}, {colour.xyz, 3 * triangle it leaves from}.
 struct QRay {
     float4 a, b, c;
 };
 struct WQ {
-    const QRay* in;           // this bounce's rays, or the handed-back rays of this bounce
+    const QRay* in;           // this bounce's rays
     const uint32_t* in_count;
     const uint32_t* perm;     // optional order of `in` (sorted), or null
-    QRay* out;                // next bounce's rays
+    QRay* out;                // next bounce's rays (null: none)
     uint32_t* out_count;
     uint32_t* fetch;          // dynamic work counter of this launch
     int bounce;
@@ -184,7 +107,6 @@ struct Outputs {
     unsigned long long* overflow;
     uint32_t* restarts;          // traversals that outgrew the LDS stack and restarted (general code)
     uint64_t local_pixels;
-    uint32_t* wave_times;        // RTK_WAVE_TIMES diagnostic: per pixel {start, end, hw_id, xcc_id}
 };
 
 __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
@@ -203,8 +125,6 @@ struct Stack {
     uint32_t* lds;      // this lane's column: lds[i * 64]
     uint32_t* glb;      // this pixel's column: glb[(i - kLdsStack) * gstride]
     uint64_t gstride;
-    const float4* nc = nullptr;   // LDS copy of inner records 0 .. ncn-1 (fast traversal), or none
-    uint32_t ncn = 0;
     __device__ __forceinline__ uint32_t get(int i) const {
         return i < kLdsStack ? lds[i * 64] : glb[(uint64_t)(i - kLdsStack) * gstride];
     }
@@ -214,22 +134,224 @@ struct Stack {
     }
 };
 
+// local row -> frame row under rt_tiling (bands of band_rows rows, band b -> rank b % nranks)
+__device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
+    if (F.nranks <= 1) return lr;
+    const uint32_t band = lr / (uint32_t)F.band_rows, rib = lr % (uint32_t)F.band_rows;
+    return (band * (uint32_t)F.nranks + (uint32_t)F.rank) * (uint32_t)F.band_rows + rib;
+}
+
+__device__ __forceinline__ uint32_t block_tile(const Frame& F) { return F.tile_order[blockIdx.x]; }
+
+// Lane -> pixel inside a block's 16x16 pixels: wave w holds 8x8 tile (w % 2, w / 2), lanes
+// in Morton order.  The vector-memory path merges the requests of the four lanes of a quad
+// that read the same record (measured 3.7x cheaper per lane than four distinct records,
+// scripts/micro/share_fetch.hip), so every quad is a 2x2 pixel square, the pixels most
+// likely to walk the same nodes.  Which lane holds which pixel never changes results.
+__device__ __forceinline__ void tile_pixel(const Frame& F, uint32_t tb, int wave, int l, uint32_t& x, uint32_t& lr) {
+    const uint32_t tx = tb % F.tiles_x, ty = tb / F.tiles_x;
+    const uint32_t lx = (uint32_t)((l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4));
+    const uint32_t ly = (uint32_t)(((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4));
+    x = tx * kBlockPx + (uint32_t)(wave & 1) * 8u + lx;
+    lr = ty * kBlockPx + (uint32_t)(wave >> 1) * 8u + ly;
+}
+
+// The frame's counters come in two parity sets; frame f uses set f & 1 and clears the
+// other one for frame f + 1 on the same stream (the kernels of f never touch it), so no
+// launch is spent on zeroing.
+__device__ __forceinline__ void zero_next_counters(const Frame& F) {
+    const uint32_t n = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < F.nzero; i += n) F.zero_next[i] = 0u;
+}
+
+// Wave-aggregated append: lanes with `want` get consecutive slots of `q`.
+__device__ __forceinline__ void wf_append(bool want, QRay* q, uint32_t* count, const QRay& r) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(want);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__builtin_popcountll(m));
+    base = __shfl(base, leader);
+    if (want) {
+        const uint32_t slot = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        q[slot] = r;
+    }
+}
+
+// Longest-first block order (LPT list scheduling): the hardware hands blocks to free CU
+// slots in blockIdx order, so dispatching the blocks that took longest last frame first
+// leaves only short blocks for the tail.  Key: log2 of the cost with 3 mantissa bits
+// (256 buckets, largest first).
+__device__ __forceinline__ uint32_t lpt_key(uint32_t c) {
+    if (c == 0) return 0;
+    const uint32_t e = 31u - __builtin_clz(c);
+    const uint32_t m = e >= 3 ? (c >> (e - 3)) & 7u : (c << (3 - e)) & 7u;
+    return min(255u, e * 8u + m);
+}
+
+// End of every block of a frame's tile kernel (all 256 threads).  The block's wall time
+// (max over its waves) goes to tile_cost[tb]; the block that finishes last sorts all of
+// them into the next frame's order (a 256-bucket counting sort), so the order costs no
+// launch of its own.  Inter-workgroup hand-off (MI355X_MICROARCH.md, visibility table
+// row 1): one lane per block stores its cost write-through (sc1), waits for the store,
+// then adds to one agent-scope counter; the block whose add returns num_blocks - 1 is
+// last, acquires, and reads every cost with sc1 loads.  `scratch` is >= 772 words of
+// LDS that no wave uses any more (the traversal stacks).
+__device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uint32_t* scratch) {
+    if (!F.tile_cost) return;   // launch-uniform
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    __syncthreads();   // every wave is done with the stacks
+    if (lane == 0) scratch[wave] = t_end - t_start + 1u;
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t c = max(max(scratch[0], scratch[1]), max(scratch[2], scratch[3]));
+        __hip_atomic_store(F.tile_cost + tb, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prev = __hip_atomic_fetch_add(F.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        scratch[4] = prev + 1u == F.num_blocks ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!scratch[4]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    uint32_t* hist = scratch + 8;      // [256]
+    uint32_t* scan = hist + 256;       // [2][256]
+    const uint32_t nb = F.num_blocks;
+    hist[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < nb; i += 256)
+        atomicAdd(&hist[lpt_key(__hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))], 1u);
+    __syncthreads();
+    // exclusive prefix over the buckets, largest key first (Hillis-Steele on 256 lanes)
+    scan[tid] = hist[255 - tid];
+    __syncthreads();
+    int src = 0;
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        scan[(src ^ 1) * 256 + tid] = scan[src * 256 + tid] + (tid >= off ? scan[src * 256 + tid - off] : 0u);
+        __syncthreads();
+        src ^= 1;
+    }
+    hist[255 - tid] = scan[src * 256 + tid] - hist[255 - tid];   // inclusive -> exclusive
+    __syncthreads();
+    for (uint32_t i = tid; i < nb; i += 256) {
+        const uint32_t c = __hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        F.lpt_next[atomicAdd(&hist[lpt_key(c)], 1u)] = i;
+    }
+    if (tid == 0) __hip_atomic_store(F.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- math-independent kernels ----
+
+// Per-bounce ray sort of the wavefront path (RT_FLAG_WF_SORT): counting sort of the
+// queue's live entries by an 8-bit key, the direction octant (3 bits) above the top 5
+// bits of the leaf position of the triangle the ray leaves from (coarsened to 13 bits by
+// the host's shift), so that a wave's rays start close together and travel the same way.
+// wf_hist_kernel: per-block LDS histogram -> global hist[256]; stores each entry's key.
+// wf_scatter_kernel: every block takes a contiguous range of each bucket for its own
+// entries (one atomic on the bucket's cursor past the exclusive prefix of hist) and
+// writes the entries' indices there, so perm[0..n) lists the queue bucket by bucket.
+// The order inside a bucket varies from run to run; pixels do not depend on it (each
+// queued ray is traced on its own), only the lanes' grouping does.
+__device__ __forceinline__ uint32_t wf_key8(const QRay& r, const uint32_t* __restrict__ rank, uint32_t shift) {
+    const int hit = __float_as_int(r.c.w);
+    const uint32_t oct = (r.b.x < 0.0f ? 4u : 0u) | (r.b.y < 0.0f ? 2u : 0u) | (r.b.z < 0.0f ? 1u : 0u);
+    const uint32_t pos13 = hit >= 0 ? min(rank[hit / 3] >> shift, 0x1FFEu) : 0x1FFEu;
+    return (oct << 5) | (pos13 >> 8);
+}
+
+__global__ void __launch_bounds__(256) wf_hist_kernel(const QRay* __restrict__ q, const uint32_t* __restrict__ count,
+                                                      const uint32_t* __restrict__ rank, uint32_t shift,
+                                                      uint8_t* __restrict__ keys, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t k = wf_key8(q[i], rank, shift);
+        keys[i] = (uint8_t)k;
+        atomicAdd(&h[k], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) wf_scatter_kernel(const uint32_t* __restrict__ count,
+                                                         const uint8_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor,
+                                                         uint32_t* __restrict__ perm) {
+    __shared__ uint32_t pre[256], h[256];
+    const uint32_t t = threadIdx.x;
+    pre[t] = hist[t];
+    h[t] = 0u;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {   // inclusive scan (Hillis-Steele)
+        const uint32_t v = t >= d ? pre[t - d] : 0u;
+        __syncthreads();
+        pre[t] += v;
+        __syncthreads();
+    }
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * 256u + t; i < n; i += gridDim.x * 256u) atomicAdd(&h[keys[i]], 1u);
+    __syncthreads();
+    const uint32_t mine = h[t];
+    const uint32_t base = pre[t] - hist[t] + (mine ? atomicAdd(&cursor[t], mine) : 0u);
+    __syncthreads();
+    pre[t] = base;
+    h[t] = 0u;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * 256u + t; i < n; i += gridDim.x * 256u) {
+        const uint32_t k = keys[i];
+        perm[pre[k] + atomicAdd(&h[k], 1u)] = i;
+    }
+}
+
+// Band re-interleave on rank 0 (rt_assemble_bands): one block per frame row,
+// 16-B copies when rows and slots are 16-B aligned.  Pure HBM copy: 8 B/pixel.
+__global__ void __launch_bounds__(256) assemble_bands_kernel(uint32_t* __restrict__ frame,
+                                                             const uint32_t* __restrict__ slots, uint64_t slot_pixels,
+                                                             uint32_t w, uint32_t h, uint32_t nranks,
+                                                             uint32_t band_rows) {
+    const uint32_t y = blockIdx.x;
+    if (y >= h) return;
+    const uint32_t band = y / band_rows;
+    const uint32_t rank = band % nranks;
+    const uint64_t local_row = (uint64_t)(band / nranks) * band_rows + (y % band_rows);
+    const uint32_t* src = slots + (uint64_t)rank * slot_pixels + local_row * w;
+    uint32_t* dst = frame + (uint64_t)y * w;
+    if ((w & 3u) == 0 && (slot_pixels & 3u) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
 }  // namespace rtk
 
-// Two instantiations of the math + kernel: S_strict (default, CPU-reproducible)
-// and S_hw (RT_FLAG_HW_MATH: the device-library rsqrt/pow the reference links).
+// Three instantiations of the math + kernels:
+//   rtk_ref    (default)            S_ref: the reference as its host builds it
+//   rtk_strict (RT_FLAG_STRICT_MATH) S_strict: CPU-reproducible, the oracle's arithmetic
+//   rtk_hw     (RT_FLAG_HW_MATH)     S_hw: the reference built with correctly rounded / and sqrt
 #define RTK_NS rtk_strict
-#define RTK_HWMATH 0
+#define RTK_MATH 0
 #include "rt_device_math.h"
 #include "rt_kernel_body.inc"
 #undef RTK_NS
-#undef RTK_HWMATH
+#undef RTK_MATH
 #define RTK_NS rtk_hw
-#define RTK_HWMATH 1
+#define RTK_MATH 1
 #include "rt_device_math.h"
 #include "rt_kernel_body.inc"
 #undef RTK_NS
-#undef RTK_HWMATH
+#undef RTK_MATH
+#define RTK_NS rtk_ref
+#define RTK_MATH 2
+#include "rt_device_math.h"
+#include "rt_kernel_body.inc"
+#undef RTK_NS
+#undef RTK_MATH
 
 // ============================================================================
 // Host side: context, upload/repack, launch.
@@ -268,34 +390,34 @@ struct rt_ctx {
     struct FrameSlot {
         void* stream = nullptr;
         uint64_t last_use = 0;
+        hipEvent_t idle = nullptr;                                          // recorded after each frame
+        uint64_t nframe = 0;                                                // frames rendered on this slot
         uint32_t* d_gstack = nullptr; size_t gstack_cap = 0;                // in pixels
         float4* d_wq[2] = {nullptr, nullptr}; size_t wq_cap[2] = {0, 0};   // wavefront ray queues (ping-pong)
-        uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // frame counters (kCounters)
-        uint32_t* d_sort[4] = {nullptr, nullptr, nullptr, nullptr}; size_t sort_cap[4] = {0, 0, 0, 0};
-        uint8_t* d_sort_tmp = nullptr; size_t sort_tmp_cap = 0;
-        uint32_t* d_cost = nullptr; size_t cost_cap = 0;   // adaptive order: last frame's per-tile times
-        uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;     //   and the longest-first order built from them
+        uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // frame counters, 2 parity sets
+        uint8_t* d_keys = nullptr; size_t keys_cap = 0;                     // wavefront sort: keys, permutation
+        uint32_t* d_perm = nullptr; size_t perm_cap = 0;
+        uint32_t* d_cost = nullptr; size_t cost_cap = 0;   // adaptive order: per-tile times,
+        uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;     //   the longest-first order built from them,
+        uint32_t* d_done = nullptr;                        //   and the finished-block counter
         uint64_t cost_key = 0; bool cost_ready = false;
     };
     static constexpr int kMaxSlots = 8;
     std::vector<FrameSlot> slots;
     FrameSlot* last_slot = nullptr;
     uint64_t slot_clock = 0;
-    uint32_t* d_rank = nullptr;                                         // triangle -> first leaf position
-    uint32_t* d_wt = nullptr; size_t wt_cap = 0;             // RTK_WAVE_TIMES
-    uint32_t* d_order = nullptr; size_t order_cap = 0;        // tile order table for the fused kernel
-    uint32_t order_tx = 0, order_ty = 0; int order_policy = -1;
+    uint32_t* d_rank = nullptr;                               // triangle -> first leaf position
+    uint32_t* d_order = nullptr; size_t order_cap = 0;        // static block order (column strips)
+    uint32_t order_tx = 0, order_ty = 0;
     uint32_t scene_gen = 0;                                   // bumped by every upload
-    int wf_grid[2] = {0, 0};   // persistent wavefront grid [strict, hw]
-    int fb_grid[2] = {0, 0};   // persistent first_bounce_kernel grid [strict, hw]
-    float last_ms = 0.0f;
+    int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
     bool timing_valid = false;
     std::string err;
 };
 
 static std::string g_err;
 
-// frame counter buffer (d_wcnt): 8 per bounce, then the restart count, then per bounce
+// frame counters (one parity set): 8 per bounce, then the restart count, then per bounce
 // the counting sort's bucket histogram and cursors (256 + 256)
 constexpr size_t kRestartSlot = 8 * (RT_MAX_DEPTH + 1);
 constexpr size_t kSortSlot = kRestartSlot + 1;
@@ -323,46 +445,41 @@ static int ensure(rt_ctx* c, T*& p, size_t& cap, size_t n) {
     return RT_OK;
 }
 
-// Per-bounce ray sort of the wavefront path (RTK_SORT_BITS of 32-bit keys, 32-bit payloads).
-static hipError_t rtk_sort_temp_bytes(int n, size_t& bytes) {
-    return hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, RTK_SORT_BITS);
-}
-static hipError_t rtk_sort_pairs(uint8_t* tmp, size_t bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
-                                 uint32_t* vout, int n, hipStream_t s) {
-    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, RTK_SORT_BITS, s);
-}
-
 static void free_slot(rt_ctx::FrameSlot& f) {
-    for (void* p : {(void*)f.d_gstack, (void*)f.d_wq[0], (void*)f.d_wq[1], (void*)f.d_wcnt, (void*)f.d_sort[0],
-                    (void*)f.d_sort[1], (void*)f.d_sort[2], (void*)f.d_sort[3], (void*)f.d_sort_tmp, (void*)f.d_cost,
-                    (void*)f.d_lpt})
+    for (void* p : {(void*)f.d_gstack, (void*)f.d_wq[0], (void*)f.d_wq[1], (void*)f.d_wcnt, (void*)f.d_keys,
+                    (void*)f.d_perm, (void*)f.d_cost, (void*)f.d_lpt, (void*)f.d_done})
         if (p) (void)hipFree(p);
+    if (f.idle) (void)hipEventDestroy(f.idle);
     f = rt_ctx::FrameSlot{};
 }
 
 // The frame scratch of `stream` (created on first use; beyond kMaxSlots streams the
-// least recently used slot is recycled after its stream has drained).
-static rt_ctx::FrameSlot* slot_for(rt_ctx* c, void* stream) {
+// least recently used slot is recycled once its last frame has finished -- waited on
+// through the slot's own event, the stream itself may be gone by then).
+static int slot_for(rt_ctx* c, void* stream, rt_ctx::FrameSlot** out) {
     ++c->slot_clock;
     for (auto& f : c->slots)
-        if (f.stream == stream) { f.last_use = c->slot_clock; return &f; }
+        if (f.stream == stream) { f.last_use = c->slot_clock; *out = &f; return RT_OK; }
     if ((int)c->slots.size() < rt_ctx::kMaxSlots) {
         c->slots.reserve(rt_ctx::kMaxSlots);   // slot pointers stay valid
         c->slots.emplace_back();
-        c->slots.back().stream = stream;
-        c->slots.back().last_use = c->slot_clock;
-        return &c->slots.back();
+        rt_ctx::FrameSlot& f = c->slots.back();
+        f.stream = stream;
+        f.last_use = c->slot_clock;
+        HIPC(c, hipEventCreateWithFlags(&f.idle, hipEventDisableTiming));
+        *out = &f;
+        return RT_OK;
     }
     rt_ctx::FrameSlot* lru = &c->slots[0];
     for (auto& f : c->slots)
         if (f.last_use < lru->last_use) lru = &f;
-    (void)hipStreamSynchronize((hipStream_t)lru->stream);
+    HIPC(c, hipEventSynchronize(lru->idle));
     lru->stream = stream;
     lru->cost_key = 0;
     lru->cost_ready = false;
     lru->last_use = c->slot_clock;
-    return lru;
+    *out = lru;
+    return RT_OK;
 }
 
 static void free_scene(rt_ctx* c) {
@@ -375,25 +492,14 @@ static void free_scene(rt_ctx* c) {
     c->have_scene = false;
 }
 
-// Block -> tile order of the fused kernel.  Blocks b, b+8, b+16, ... run on one
-// XCD (round-robin dispatch; a speed assumption only, never correctness).
-//   policy 0: none (in-kernel chunk dealing, RTK_XCD_CHUNK)
-//   policy 1: column strips -- XCD k gets the k-th eighth of the tile columns and
-//             walks it row by row, so all XCDs sweep the frame bottom-up together
-//             (balanced) while each L2 sees one compact screen region.
-static int tile_order_policy() {
-    const char* e = std::getenv("RTAMD_TILE_ORDER");
-    return e ? std::atoi(e) : RTK_TILE_ORDER;
-}
-
-static std::vector<uint32_t> tile_order_table(uint32_t tx, uint32_t ty, int policy) {
+// Static block -> tile order (the first frame of a geometry, and RT_FLAG_STATIC_ORDER).
+// Blocks b, b+8, b+16, ... run on one XCD (round-robin dispatch; a speed assumption
+// only, never correctness): XCD k gets the k-th eighth of the tile columns and walks it
+// row by row, so all XCDs sweep the frame bottom-up together (balanced) while each L2
+// sees one compact screen region.
+static std::vector<uint32_t> tile_order_table(uint32_t tx, uint32_t ty) {
     const uint32_t nb = tx * ty;
     std::vector<uint32_t> order(nb);
-    if (policy != 1) {
-        for (uint32_t b = 0; b < nb; ++b) order[b] = b;
-        return order;
-    }
-    // per-XCD tile lists: XCD k owns columns [k*tx/8, (k+1)*tx/8), row-major within its strip
     std::vector<std::vector<uint32_t>> want(8);
     for (uint32_t k = 0; k < 8; ++k) {
         const uint32_t c0 = k * tx / 8, c1 = (k + 1) * tx / 8;
@@ -418,31 +524,37 @@ static std::vector<uint32_t> tile_order_table(uint32_t tx, uint32_t ty, int poli
     return order;
 }
 
-// Band re-interleave on rank 0 (rt_assemble_bands): one block per frame row,
-// 16-B copies when rows and slots are 16-B aligned.  Pure HBM copy: 8 B/pixel.
-__global__ void __launch_bounds__(256) assemble_bands_kernel(uint32_t* __restrict__ frame,
-                                                             const uint32_t* __restrict__ slots, uint64_t slot_pixels,
-                                                             uint32_t w, uint32_t h, uint32_t nranks,
-                                                             uint32_t band_rows) {
-    const uint32_t y = blockIdx.x;
-    if (y >= h) return;
-    const uint32_t band = y / band_rows;
-    const uint32_t rank = band % nranks;
-    const uint64_t local_row = (uint64_t)(band / nranks) * band_rows + (y % band_rows);
-    const uint32_t* src = slots + (uint64_t)rank * slot_pixels + local_row * w;
-    uint32_t* dst = frame + (uint64_t)y * w;
-    if ((w & 3u) == 0 && (slot_pixels & 3u) == 0) {
-        const uint4* s4 = reinterpret_cast<const uint4*>(src);
-        uint4* d4 = reinterpret_cast<uint4*>(dst);
-        for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
-    } else {
-        for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) dst[i] = src[i];
-    }
+// Kernels of one math mode (namespace NS), picked at launch by the frame's flags.
+template <int M> struct Kernels;
+#define RTK_KERNELS(M, NS)                                                                                 \
+    template <> struct Kernels<M> {                                                                        \
+        static void* first(bool fast, bool next) {                                                        \
+            return fast ? (next ? (void*)NS::first_bounce_kernel<true, true> : (void*)NS::first_bounce_kernel<true, false>) \
+                        : (next ? (void*)NS::first_bounce_kernel<false, true> : (void*)NS::first_bounce_kernel<false, false>); \
+        }                                                                                                  \
+        static void* fused(bool fast) { return fast ? (void*)NS::render_kernel<true> : (void*)NS::render_kernel<false>; } \
+        static void* bounce(bool fast) {                                                                   \
+            return fast ? (void*)NS::wf_bounce_kernel<true> : (void*)NS::wf_bounce_kernel<false>;          \
+        }                                                                                                  \
+    };
+RTK_KERNELS(0, rtk_strict)
+RTK_KERNELS(1, rtk_hw)
+RTK_KERNELS(2, rtk_ref)
+#undef RTK_KERNELS
+
+static void* kernel_first(int m, bool fast, bool next) {
+    return m == 0 ? Kernels<0>::first(fast, next) : m == 1 ? Kernels<1>::first(fast, next) : Kernels<2>::first(fast, next);
+}
+static void* kernel_fused(int m, bool fast) {
+    return m == 0 ? Kernels<0>::fused(fast) : m == 1 ? Kernels<1>::fused(fast) : Kernels<2>::fused(fast);
+}
+static void* kernel_bounce(int m, bool fast) {
+    return m == 0 ? Kernels<0>::bounce(fast) : m == 1 ? Kernels<1>::bounce(fast) : Kernels<2>::bounce(fast);
 }
 
 extern "C" {
 
-int rt_abi_version(void) { return 1; }
+int rt_abi_version(void) { return 2; }
 
 int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint32_t w, uint32_t h,
                       int32_t nranks, int32_t band_rows, void* stream) {
@@ -454,7 +566,7 @@ int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_
         return set_err(nullptr, "rt_assemble_bands: slot_pixels smaller than rank 0's bands", RT_ERR_INVALID_ARG);
     if (((uintptr_t)d_frame | (uintptr_t)d_slots) & 15u)
         return set_err(nullptr, "rt_assemble_bands: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
-    hipLaunchKernelGGL(assemble_bands_kernel, dim3(h), dim3(256), 0, (hipStream_t)stream, d_frame, d_slots,
+    hipLaunchKernelGGL(rtk::assemble_bands_kernel, dim3(h), dim3(256), 0, (hipStream_t)stream, d_frame, d_slots,
                        slot_pixels, w, h, (uint32_t)nranks, (uint32_t)band_rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(nullptr, std::string("rt_assemble_bands: ") + hipGetErrorString(e), RT_ERR_DEVICE);
@@ -473,7 +585,6 @@ int rt_create(int device, rt_ctx** out) {
     rt_ctx* c = new rt_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-
         hipMalloc((void**)&c->d_overflow, sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(c->d_overflow, 0, sizeof(unsigned long long)) != hipSuccess) {
         delete c;
@@ -487,16 +598,16 @@ int rt_destroy(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID_ARG;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& f : c->slots)
+        if (f.idle) (void)hipEventSynchronize(f.idle);   // frames may still run on caller streams
     free_scene(c);
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_hits) (void)hipFree(c->d_hits);
     if (c->d_t) (void)hipFree(c->d_t);
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
-    (void)hipDeviceSynchronize();   // frames may still run on caller streams
     for (auto& f : c->slots) free_slot(f);
-    for (void* p : {(void*)c->d_order, (void*)c->d_wt})
-        if (p) (void)hipFree(p);
+    if (c->d_order) (void)hipFree(c->d_order);
     for (auto& f : c->ring)
         for (hipEvent_t& e : f.e)
             if (e) (void)hipEventDestroy(e);
@@ -528,11 +639,10 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
     std::vector<int32_t> inner_id(nn, -1);
     std::vector<int2> leaf_table;
     std::vector<uint32_t> ref_of(nn, 0);
-    std::vector<int64_t> leaf_pos(nn, -1);   // RTK_QUAD_SYNC: a reachable leaf's first triangle record
     // inner ids in pre-order of reachability from the root; detect cycles (the
     // reference would spin forever on some of them).
+    std::vector<uint8_t> state(nn, 0);  // 0 new, 1 on path, 2 done
     {
-        std::vector<uint8_t> state(nn, 0);  // 0 new, 1 on path, 2 done
         std::vector<std::pair<int32_t, int>> stk;
         int32_t next = 0;
         stk.push_back({0, 0});
@@ -558,166 +668,127 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             state[n] = 2;
             stk.pop_back();
         }
-        // RTK_QUAD_SYNC: inner records and the triangle records of each reachable leaf take
-        // their position in the left-first depth-first order of the reachable tree (one
-        // index space for both arrays), so a ref is its own DFS key (rt_kernel_body.inc
-        // traverse_ifif).  Otherwise: the first kBfsTop inner nodes in breadth-first order
-        // from the root get ids 0..kBfsTop-1 (the top of the tree, which every ray walks:
-        // the fast kernel keeps the first RTK_NODE_CACHE of them in LDS); the rest keep
-        // their pre-order.
-#if RTK_QUAD_SYNC
-        {
-            std::vector<int32_t> dfs{0};
-            std::vector<uint8_t> seen(nn, 0);
-            int64_t pos = 0;
-            while (!dfs.empty()) {
-                const int32_t n = dfs.back();
-                dfs.pop_back();
-                if (seen[n]) continue;
-                seen[n] = 1;
-                const rt_bvh_node& nd = nodes[n];
-                if (inner_id[n] >= 0) {
-                    inner_id[n] = (int32_t)pos++;
-                    dfs.push_back(nd.offset_right);
-                    dfs.push_back(nd.offset_left);
-                } else if (nd.offset_left < 0) {
-                    leaf_pos[n] = pos;
-                    pos += nd.num_tris < 0 ? 0 : nd.num_tris;
+        // the first kBfsTop inner nodes in breadth-first order from the root get ids
+        // 0..kBfsTop-1 (the top of the tree, which every ray walks, in 64 KB); the rest
+        // keep their pre-order
+        constexpr int32_t kBfsTop = 1024;
+        std::vector<int32_t> bfs;
+        std::vector<uint8_t> seen(nn, 0);
+        if (inner_id[0] >= 0) { bfs.push_back(0); seen[0] = 1; }
+        for (size_t i = 0; i < bfs.size() && (int32_t)bfs.size() < kBfsTop; ++i) {
+            const rt_bvh_node& nd = nodes[bfs[i]];
+            for (int32_t ch : {nd.offset_left, nd.offset_right})
+                if (inner_id[ch] >= 0 && !seen[ch] && (int32_t)bfs.size() < kBfsTop) {
+                    seen[ch] = 1;
+                    bfs.push_back(ch);
                 }
-                if (pos >= (int64_t)1 << 30) return set_err(c, "BVH too large for the DFS layout", RT_ERR_BAD_SCENE);
-            }
-            next = (int32_t)pos;
         }
-#else
-        {
-            constexpr int32_t kBfsTop = 1024;
-            std::vector<int32_t> bfs;
-            std::vector<uint8_t> seen(nn, 0);
-            if (inner_id[0] >= 0) { bfs.push_back(0); seen[0] = 1; }
-            for (size_t i = 0; i < bfs.size() && (int32_t)bfs.size() < kBfsTop; ++i) {
-                const rt_bvh_node& nd = nodes[bfs[i]];
-                for (int32_t ch : {nd.offset_left, nd.offset_right})
-                    if (inner_id[ch] >= 0 && !seen[ch] && (int32_t)bfs.size() < kBfsTop) {
-                        seen[ch] = 1;
-                        bfs.push_back(ch);
-                    }
-            }
-            std::vector<int32_t> by_old(next, -1);
-            for (int32_t n = 0; n < nn; ++n)
-                if (inner_id[n] >= 0) by_old[inner_id[n]] = n;
-            int32_t id = 0;
-            for (int32_t n : bfs) inner_id[n] = id++;
-            for (int32_t o = 0; o < next; ++o)
-                if (!seen[by_old[o]]) inner_id[by_old[o]] = id++;
-        }
-#endif
-        bool clean = true;
+        std::vector<int32_t> by_old(next, -1);
         for (int32_t n = 0; n < nn; ++n)
-            if (state[n] != 0 && nodes[n].offset_left >= 0 && inner_id[n] < 0) clean = false;
-        c->clean = clean ? 1 : 0;
-        for (int32_t n = 0; n < nn; ++n) {
-            const rt_bvh_node& nd = nodes[n];
-            if (nd.offset_left >= 0) {
-                ref_of[n] = inner_id[n] >= 0 ? (uint32_t)inner_id[n] : rtk::kRefError;
-            } else {
-                int32_t off = nd.offset_tris, cnt = nd.num_tris < 0 ? 0 : nd.num_tris;
-                if (cnt > 0 && (off < 0 || (int64_t)off + cnt > nref))
-                    return set_err(c, "leaf triangle range out of bounds", RT_ERR_BAD_SCENE);
-                if (cnt == 0) off = 0;
-                if (RTK_QUAD_SYNC) off = leaf_pos[n] < 0 ? 0 : (int32_t)leaf_pos[n];
-                if (cnt < (int32_t)rtk::kCntEscape && off < (1 << 26)) {
-                    ref_of[n] = rtk::kLeafBit | ((uint32_t)cnt << 26) | (uint32_t)off;
-                } else {
-                    if (leaf_table.size() >= (1u << 26)) return set_err(c, "too many escape leaves", RT_ERR_BAD_SCENE);
-                    ref_of[n] = rtk::kLeafBit | (rtk::kCntEscape << 26) | (uint32_t)leaf_table.size();
-                    leaf_table.push_back(make_int2(off, cnt));
-                }
-            }
-        }
-        int32_t n_inner = next;
-        std::vector<float4> wn((size_t)std::max(n_inner, 1) * 4, make_float4(0, 0, 0, 0));
-        bool fast_ok = true;  // slab-test fast exact division domain (rt_kernel_body.inc axis_ok)
-        for (int32_t n = 0; n < nn; ++n) {
-            if (inner_id[n] < 0) continue;
-            const rt_bvh_node& L = nodes[nodes[n].offset_left];
-            const rt_bvh_node& R = nodes[nodes[n].offset_right];
-            float4* q = &wn[(size_t)inner_id[n] * 4];
-            // axis-major: {L.min, R.min, L.max, R.max} per axis (rt_kernel_body.inc slab2)
-            q[0] = make_float4(L.min.x, R.min.x, L.max.x, R.max.x);
-            q[1] = make_float4(L.min.y, R.min.y, L.max.y, R.max.y);
-            q[2] = make_float4(L.min.z, R.min.z, L.max.z, R.max.z);
-            uint32_t r0 = ref_of[nodes[n].offset_left], r1 = ref_of[nodes[n].offset_right];
-            float f0, f1;
-            std::memcpy(&f0, &r0, 4);
-            std::memcpy(&f1, &r1, 4);
-            q[3] = make_float4(f0, f1, 0.0f, 0.0f);
-            for (int k = 0; k < 3; ++k) {
-                const float* qf = &q[k].x;
-                for (int j = 0; j < 4; ++j) {
-                    const float a = std::fabs(qf[j]);
-                    if (!(a == 0.0f || (a >= 0x1p-66f && a <= 0x1p60f))) fast_ok = false;
-                }
-            }
-        }
-        // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974)
-        // + a 16-B tail pad: traverse_ifif fetches 64 B at a triangle record (48 B used)
-        // (RTK_QUAD_SYNC: each reachable leaf's references copied to its DFS positions)
-        const int32_t ntrec = RTK_QUAD_SYNC ? n_inner : nref;
-        std::vector<float4> tr((size_t)std::max(ntrec, 1) * 3 + 1, make_float4(0, 0, 0, 0));
-        auto put_tri = [&](int64_t at, int32_t tri1) {
-            const rt_float4 v0 = verts[idx[tri1]], v1 = verts[idx[tri1 + 1]], v2 = verts[idx[tri1 + 2]];
-            float idf;
-            std::memcpy(&idf, &tri1, 4);
-            tr[(size_t)at * 3 + 0] = make_float4(v0.x, v0.y, v0.z, idf);
-            tr[(size_t)at * 3 + 1] = make_float4(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z, 0.0f);
-            tr[(size_t)at * 3 + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.0f);
-        };
-        if (RTK_QUAD_SYNC) {
-            for (int32_t n = 0; n < nn; ++n)
-                if (leaf_pos[n] >= 0)
-                    for (int32_t i = 0; i < nodes[n].num_tris; ++i) put_tri(leaf_pos[n] + i, refs[nodes[n].offset_tris + i]);
-        } else {
-            for (int32_t i = 0; i < nref; ++i) put_tri(i, refs[i]);
-        }
-        // per-triangle shading records (volumeRender.cl:1306-1374)
-        std::vector<float4> sh((size_t)ntri * 7);
-        for (int32_t t = 0; t < ntri; ++t) {
-            float4* s = &sh[(size_t)t * 7];
-            for (int k = 0; k < 3; ++k) {
-                const rt_float4 v = verts[idx[3 * t + k]];
-                const rt_float4 n = normals[normal_idx[3 * t + k]];
-                s[k] = make_float4(v.x, v.y, v.z, 0.0f);
-                s[3 + k] = make_float4(n.x, n.y, n.z, 0.0f);
-            }
-            const rt_float4 d = mats[tri_to_mat[t]].diffuse;
-            s[6] = make_float4(d.x, d.y, d.z, 0.0f);
-        }
-        if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
-
-        HIPC(c, hipSetDevice(c->device));
-        free_scene(c);
-        HIPC(c, hipMalloc((void**)&c->d_wnodes, wn.size() * sizeof(float4)));
-        HIPC(c, hipMalloc((void**)&c->d_tris, tr.size() * sizeof(float4)));
-        HIPC(c, hipMalloc((void**)&c->d_shade, sh.size() * sizeof(float4)));
-        HIPC(c, hipMalloc((void**)&c->d_leaf, leaf_table.size() * sizeof(int2)));
-        HIPC(c, hipMemcpy(c->d_wnodes, wn.data(), wn.size() * sizeof(float4), hipMemcpyHostToDevice));
-        HIPC(c, hipMemcpy(c->d_tris, tr.data(), tr.size() * sizeof(float4), hipMemcpyHostToDevice));
-        {   // triangle -> position of its first reference in leaf order (wavefront sort keys)
-            std::vector<uint32_t> rank((size_t)std::max(ntri, 1), 0x1FFFFFFEu);
-            for (int32_t i = nref - 1; i >= 0; --i) rank[(size_t)(refs[i] / 3)] = (uint32_t)i;
-            HIPC(c, hipMalloc((void**)&c->d_rank, rank.size() * sizeof(uint32_t)));
-            HIPC(c, hipMemcpy(c->d_rank, rank.data(), rank.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        }
-        HIPC(c, hipMemcpy(c->d_shade, sh.data(), sh.size() * sizeof(float4), hipMemcpyHostToDevice));
-        HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
-        c->root = ref_of[0];
-        c->n_inner = (uint32_t)n_inner;
-        c->rank_shift = 0;
-        while (((uint64_t)std::max(nref, 1) >> c->rank_shift) > 0x1FFEu) ++c->rank_shift;
-        c->fast_div = fast_ok ? 1 : 0;
-        c->have_scene = true;
-        ++c->scene_gen;
+            if (inner_id[n] >= 0) by_old[inner_id[n]] = n;
+        int32_t id = 0;
+        for (int32_t n : bfs) inner_id[n] = id++;
+        for (int32_t o = 0; o < next; ++o)
+            if (!seen[by_old[o]]) inner_id[by_old[o]] = id++;
     }
+    bool clean = true;
+    for (int32_t n = 0; n < nn; ++n)
+        if (state[n] != 0 && nodes[n].offset_left >= 0 && inner_id[n] < 0) clean = false;
+    int32_t n_inner = 0;
+    for (int32_t n = 0; n < nn; ++n) {
+        const rt_bvh_node& nd = nodes[n];
+        if (inner_id[n] >= 0) ++n_inner;
+        if (nd.offset_left >= 0) {
+            ref_of[n] = inner_id[n] >= 0 ? (uint32_t)inner_id[n] : rtk::kRefError;
+        } else {
+            int32_t off = nd.offset_tris, cnt = nd.num_tris < 0 ? 0 : nd.num_tris;
+            if (cnt > 0 && (off < 0 || (int64_t)off + cnt > nref))
+                return set_err(c, "leaf triangle range out of bounds", RT_ERR_BAD_SCENE);
+            if (cnt == 0) off = 0;
+            if (cnt < (int32_t)rtk::kCntEscape && off < (1 << 26)) {
+                ref_of[n] = rtk::kLeafBit | ((uint32_t)cnt << 26) | (uint32_t)off;
+            } else {
+                if (leaf_table.size() >= (1u << 26)) return set_err(c, "too many escape leaves", RT_ERR_BAD_SCENE);
+                ref_of[n] = rtk::kLeafBit | (rtk::kCntEscape << 26) | (uint32_t)leaf_table.size();
+                leaf_table.push_back(make_int2(off, cnt));
+            }
+        }
+    }
+    std::vector<float4> wn((size_t)std::max(n_inner, 1) * 4, make_float4(0, 0, 0, 0));
+    bool fast_ok = true;  // slab-test fast quotient domain (rt_kernel_body.inc axis_ok)
+    for (int32_t n = 0; n < nn; ++n) {
+        if (inner_id[n] < 0) continue;
+        const rt_bvh_node& L = nodes[nodes[n].offset_left];
+        const rt_bvh_node& R = nodes[nodes[n].offset_right];
+        float4* q = &wn[(size_t)inner_id[n] * 4];
+        // axis-major: {L.min, R.min, L.max, R.max} per axis (rt_kernel_body.inc slab2_pk)
+        q[0] = make_float4(L.min.x, R.min.x, L.max.x, R.max.x);
+        q[1] = make_float4(L.min.y, R.min.y, L.max.y, R.max.y);
+        q[2] = make_float4(L.min.z, R.min.z, L.max.z, R.max.z);
+        uint32_t r0 = ref_of[nodes[n].offset_left], r1 = ref_of[nodes[n].offset_right];
+        float f0, f1;
+        std::memcpy(&f0, &r0, 4);
+        std::memcpy(&f1, &r1, 4);
+        q[3] = make_float4(f0, f1, 0.0f, 0.0f);
+        for (int k = 0; k < 3; ++k) {
+            const float* qf = &q[k].x;
+            for (int j = 0; j < 4; ++j) {
+                const float a = std::fabs(qf[j]);
+                if (!(a == 0.0f || (a >= 0x1p-66f && a <= 0x1p60f))) fast_ok = false;
+            }
+        }
+    }
+    // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974)
+    std::vector<float4> tr((size_t)std::max(nref, 1) * 3 + 1, make_float4(0, 0, 0, 0));
+    for (int32_t i = 0; i < nref; ++i) {
+        const int32_t tri1 = refs[i];
+        const rt_float4 v0 = verts[idx[tri1]], v1 = verts[idx[tri1 + 1]], v2 = verts[idx[tri1 + 2]];
+        float idf;
+        std::memcpy(&idf, &tri1, 4);
+        tr[(size_t)i * 3 + 0] = make_float4(v0.x, v0.y, v0.z, idf);
+        tr[(size_t)i * 3 + 1] = make_float4(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z, 0.0f);
+        tr[(size_t)i * 3 + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.0f);
+    }
+    // per-triangle shading records (volumeRender.cl:1306-1374)
+    std::vector<float4> sh((size_t)ntri * 7);
+    for (int32_t t = 0; t < ntri; ++t) {
+        float4* s = &sh[(size_t)t * 7];
+        for (int k = 0; k < 3; ++k) {
+            const rt_float4 v = verts[idx[3 * t + k]];
+            const rt_float4 n = normals[normal_idx[3 * t + k]];
+            s[k] = make_float4(v.x, v.y, v.z, 0.0f);
+            s[3 + k] = make_float4(n.x, n.y, n.z, 0.0f);
+        }
+        const rt_float4 d = mats[tri_to_mat[t]].diffuse;
+        s[6] = make_float4(d.x, d.y, d.z, 0.0f);
+    }
+    if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
+    // triangle -> position of its first reference in leaf order (wavefront sort keys)
+    std::vector<uint32_t> rank((size_t)std::max(ntri, 1), 0x1FFFFFFEu);
+    for (int32_t i = nref - 1; i >= 0; --i) rank[(size_t)(refs[i] / 3)] = (uint32_t)i;
+
+    HIPC(c, hipSetDevice(c->device));
+    for (auto& f : c->slots)
+        if (f.idle) HIPC(c, hipEventSynchronize(f.idle));   // frames in flight still read the old scene
+    free_scene(c);
+    HIPC(c, hipMalloc((void**)&c->d_wnodes, wn.size() * sizeof(float4)));
+    HIPC(c, hipMalloc((void**)&c->d_tris, tr.size() * sizeof(float4)));
+    HIPC(c, hipMalloc((void**)&c->d_shade, sh.size() * sizeof(float4)));
+    HIPC(c, hipMalloc((void**)&c->d_leaf, leaf_table.size() * sizeof(int2)));
+    HIPC(c, hipMalloc((void**)&c->d_rank, rank.size() * sizeof(uint32_t)));
+    HIPC(c, hipMemcpy(c->d_wnodes, wn.data(), wn.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->d_tris, tr.data(), tr.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->d_shade, sh.data(), sh.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->d_rank, rank.data(), rank.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->root = ref_of[0];
+    c->n_inner = (uint32_t)n_inner;
+    c->rank_shift = 0;
+    while (((uint64_t)std::max(nref, 1) >> c->rank_shift) > 0x1FFEu) ++c->rank_shift;
+    c->fast_div = fast_ok ? 1 : 0;
+    c->clean = clean ? 1 : 0;
+    c->have_scene = true;
+    ++c->scene_gen;
     return RT_OK;
 }
 
@@ -741,6 +812,8 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
                      uint32_t* d_out, const rt_aux* d_aux, void* stream) {
     if (!c || !d_out || w == 0 || h == 0 || depth < 0 || depth > RT_MAX_DEPTH)
         return set_err(c, "rt_render_device: invalid argument", RT_ERR_INVALID_ARG);
+    if ((flags & RT_FLAG_STRICT_MATH) && (flags & RT_FLAG_HW_MATH))
+        return set_err(c, "rt_render_device: RT_FLAG_STRICT_MATH and RT_FLAG_HW_MATH exclude each other", RT_ERR_INVALID_ARG);
     if (!c->have_scene) return set_err(c, "rt_render_device: no scene uploaded", RT_ERR_NO_SCENE);
     if (!c->have_params) return set_err(c, "rt_render_device: no params set", RT_ERR_NO_SCENE);
     rt_tiling whole{0, 1, 16, 0};
@@ -754,8 +827,11 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     if (npix == 0) return RT_OK;
     int rc = RT_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    rt_ctx::FrameSlot& L = *slot_for(c, (void*)s);
+    rt_ctx::FrameSlot* Lp = nullptr;
+    if ((rc = slot_for(c, (void*)s, &Lp))) return rc;
+    rt_ctx::FrameSlot& L = *Lp;
     c->last_slot = &L;
+    const int math = (flags & RT_FLAG_STRICT_MATH) ? 0 : (flags & RT_FLAG_HW_MATH) ? 1 : 2;
 
     rtk::Frame F;
     const rt_params& P = c->params;
@@ -774,17 +850,9 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.nranks = T->nranks > 1 ? T->nranks : 1;
     F.band_rows = T->nranks > 1 ? T->band_rows : 16;
     F.local_rows = (uint32_t)(npix / w);
-    {
-        const uint32_t bw = RTK_FUSED_WAVES >= 2 ? 16 : 8, bh = RTK_FUSED_WAVES == 4 ? 16 : 8;
-        F.tiles_x = (w + bw - 1) / bw;
-        F.tiles_y = (F.local_rows + bh - 1) / bh;
-    }
+    F.tiles_x = (w + rtk::kBlockPx - 1) / rtk::kBlockPx;
+    F.tiles_y = (F.local_rows + rtk::kBlockPx - 1) / rtk::kBlockPx;
     F.num_blocks = F.tiles_x * F.tiles_y;
-    F.work_counter = nullptr;
-    F.tiles8_x = (w + 7) / 8;
-    F.num_tiles8 = F.tiles8_x * ((F.local_rows + 7) / 8);
-    F.tile_order = nullptr;
-    F.tile_cost = nullptr;
 
     rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root, c->n_inner,
                     (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0, c->clean};
@@ -793,12 +861,9 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.hits = aux ? d_aux->hits : nullptr;
     O.t = aux ? d_aux->t : nullptr;
     O.rgb = aux ? d_aux->rgb : nullptr;
-    O.gstack = L.d_gstack;
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
-    O.wave_times = nullptr;
 
-    const bool hw = (flags & RT_FLAG_HW_MATH) != 0;
     rt_ctx::FrameEv& E = c->ring[c->frames % rt_ctx::kRing];
     for (hipEvent_t& e : E.e)
         if (!e) HIPC(c, hipEventCreate(&e));
@@ -809,194 +874,128 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
 
     if ((rc = ensure(c, L.d_gstack, L.gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
     O.gstack = L.d_gstack;
-    // frame counters: [8k + 0] queue size of bounce k, [8k + 2] its fetch cursor,
-    // [kRestartSlot] restarted traversals; zeroed by the frame's first launch
-    if ((rc = ensure(c, L.d_wcnt, L.wcnt_cap, kCounters))) return rc;
-    O.restarts = L.d_wcnt + kRestartSlot;
-#if RTK_WAVE_TIMES
-    if (std::getenv("RTAMD_WAVE_TIMES")) {
-        if ((rc = ensure(c, c->d_wt, c->wt_cap, (size_t)npix * 4))) return rc;
-        HIPC(c, hipMemsetAsync(c->d_wt, 0, (size_t)npix * 16, s));
-        O.wave_times = c->d_wt;
+    // frame counters, two parity sets: [8k + 0] queue size of bounce k, [8k + 2] its fetch
+    // cursor, [kRestartSlot] restarted traversals, then the sort histograms
+    if (!L.d_wcnt) {
+        if ((rc = ensure(c, L.d_wcnt, L.wcnt_cap, 2 * kCounters))) return rc;
+        HIPC(c, hipMemsetAsync(L.d_wcnt, 0, 2 * kCounters * sizeof(uint32_t), s));
     }
-#endif
-    // first_bounce_kernel with persistent waves schedules 8x8 tiles, the others blocks
-    const bool persistent = wavefront && RTK_PERSISTENT;
-    const uint32_t units = persistent ? F.num_tiles8 : F.num_blocks;
-    // static block order (in-kernel XCD chunk dealing, or a host-built table)
-    F.tile_order = nullptr;
-    const int pol = persistent ? 0 : tile_order_policy();
-    if (pol != 0) {
-        if (c->order_policy != pol || c->order_tx != F.tiles_x || c->order_ty != F.tiles_y) {
-            const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y, pol);
-            if ((rc = ensure(c, c->d_order, c->order_cap, tab.size()))) return rc;
-            HIPC(c, hipMemcpy(c->d_order, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
-            c->order_policy = pol;
-            c->order_tx = F.tiles_x;
-            c->order_ty = F.tiles_y;
-        }
-        F.tile_order = c->d_order;
+    const uint64_t par = L.nframe & 1u;
+    uint32_t* cnt = L.d_wcnt + par * kCounters;
+    F.zero_next = L.d_wcnt + (par ^ 1u) * kCounters;
+    F.nzero = (uint32_t)kCounters;
+    O.restarts = cnt + kRestartSlot;
+
+    // static block order: a host-built table, rebuilt when the block grid changes
+    if (c->order_tx != F.tiles_x || c->order_ty != F.tiles_y || !c->d_order) {
+        const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y);
+        HIPC(c, hipStreamSynchronize(s));   // an earlier frame on this stream may still read the table
+        for (auto& f : c->slots)
+            if (f.idle) HIPC(c, hipEventSynchronize(f.idle));
+        if ((rc = ensure(c, c->d_order, c->order_cap, tab.size()))) return rc;
+        HIPC(c, hipMemcpy(c->d_order, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+        c->order_tx = F.tiles_x;
+        c->order_ty = F.tiles_y;
     }
-    // Adaptive longest-first order (tile_order_kernel) from the previous frame of
-    // the same geometry; the first frame runs the static order and measures.
+    F.tile_order = c->d_order;
+    // Adaptive longest-first order from the previous frame of the same geometry on this
+    // slot, built by that frame's last block; the first frame runs the static order.
     F.tile_cost = nullptr;
-    bool lpt = false;
+    F.lpt_next = nullptr;
+    F.done = nullptr;
     if (!(flags & RT_FLAG_STATIC_ORDER)) {
+        const uint32_t units = F.num_blocks;
+        const bool fresh = L.cost_cap < units || !L.d_done;
         if ((rc = ensure(c, L.d_cost, L.cost_cap, units))) return rc;
         if ((rc = ensure(c, L.d_lpt, L.lpt_cap, units))) return rc;
+        if (!L.d_done) {
+            size_t one = 0;
+            if ((rc = ensure(c, L.d_done, one, 1))) return rc;
+        }
         const uint64_t key = ((uint64_t)F.tiles_x << 48) ^ ((uint64_t)F.tiles_y << 32) ^ F.local_rows ^
-                             ((uint64_t)c->scene_gen << 20) ^ (wavefront ? (1ull << 63) : 0ull) ^
-                             (persistent ? (1ull << 62) : 0ull);
-        if (key != L.cost_key) {
-            HIPC(c, hipMemsetAsync(L.d_cost, 0, (size_t)units * 4, s));
+                             ((uint64_t)c->scene_gen << 20);
+        if (fresh || key != L.cost_key) {
+            HIPC(c, hipMemsetAsync(L.d_done, 0, sizeof(uint32_t), s));
             L.cost_key = key;
             L.cost_ready = false;
         }
-        lpt = L.cost_ready;
+        if (L.cost_ready) F.tile_order = L.d_lpt;
         F.tile_cost = L.d_cost;
+        F.lpt_next = L.d_lpt;
+        F.done = L.d_done;
     }
-    const bool fast_kernel = S.clean != 0;   // any quotient domain: traverse_fast picks the variant
-    const dim3 grid(F.num_blocks), block(64 * RTK_FUSED_WAVES);
-    const int ax = aux ? 1 : 0;
+    const bool fast = S.clean != 0;   // any quotient domain: traverse_fast picks the variant
+    const dim3 grid(F.num_blocks), block(256);
+    int ax = aux ? 1 : 0;
     HIPC(c, hipEventRecord(E.e[0], s));
-    // first launch: zero the counters (all of them for the wavefront queues, else the
-    // restart count) and, with a measured previous frame, build the longest-first order
-    // A/B (env RTAMD_LPT_STRIPS=1): longest-first within 8 column strips, one per XCD, when
-    // the block columns divide evenly.  Measured slower than the global order (C3 -3 %, C2 -40 %:
-    // the strips' balance costs more than the L2 locality gains), so off by default.
-    const char* strips_env = std::getenv("RTAMD_LPT_STRIPS");
-    const uint32_t strips = (!persistent && F.tiles_x % 8u == 0 && F.tiles_x >= 8u && strips_env &&
-                             std::atoi(strips_env) != 0) ? 8u : 0u;
-    hipLaunchKernelGGL(rtk_strict::tile_order_kernel, dim3(1), dim3(256), 0, s, L.d_cost, L.d_lpt,
-                       lpt ? units : 0u, wavefront ? L.d_wcnt : L.d_wcnt + kRestartSlot,
-                       wavefront ? (uint32_t)kCounters : 1u, F.tiles_x, strips);
-    if (lpt) F.tile_order = L.d_lpt;
-    if (F.tile_cost) L.cost_ready = true;
 
     if (!wavefront) {
         HIPC(c, hipEventRecord(E.e[2], s));
-        if (fast_kernel) {
-            if (hw) hipLaunchKernelGGL(rtk_hw::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
-            else hipLaunchKernelGGL(rtk_strict::render_kernel<true>, grid, block, 0, s, S, F, O, ax);
-        } else if (hw) {
-            hipLaunchKernelGGL(rtk_hw::render_kernel<false>, grid, block, 0, s, S, F, O, ax);
-        } else {
-            hipLaunchKernelGGL(rtk_strict::render_kernel<false>, grid, block, 0, s, S, F, O, ax);
-        }
+        void* args[] = {&S, &F, &O, &ax};
+        HIPC(c, hipLaunchKernel(kernel_fused(math, fast), grid, block, args, 0, s));
         HIPC(c, hipEventRecord(E.e[3], s));
         E.has_k = true;
-        HIPC(c, hipGetLastError());
-        HIPC(c, hipEventRecord(E.e[1], s));
     } else {
         // Wavefront: bounce 0 over tiles, then one persistent launch per further bounce
         // over the queue of rays still in flight.
-        const int mi = hw ? 1 : 0;
-        if (!c->wf_grid[mi]) {
+        if (!c->wf_grid[math] && depth > 1) {
             int cus = 0, b1 = 0;
             HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-            if (hw) HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_hw::wf_bounce_kernel<true>, 256, 0));
-            else HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, rtk_strict::wf_bounce_kernel<true>, 256, 0));
-            c->wf_grid[mi] = std::max(8, std::max(b1, 1) * cus);
+            HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (const void*)kernel_bounce(math, true), 256, 0));
+            c->wf_grid[math] = std::max(8, std::max(b1, 1) * cus);
         }
         const size_t qcap = (size_t)npix * 3;  // float4 per QRay x 3
         if (depth > 1 && (rc = ensure(c, L.d_wq[0], L.wq_cap[0], qcap))) return rc;
         if (depth > 1 && (rc = ensure(c, L.d_wq[1], L.wq_cap[1], qcap))) return rc;
         const bool sort = (flags & RT_FLAG_WF_SORT) && depth > 1 && c->d_rank;
         if (sort) {
-            for (int i = 0; i < 4; ++i)
-                if ((rc = ensure(c, L.d_sort[i], L.sort_cap[i], (size_t)npix))) return rc;
-            size_t need = 0;
-            HIPC(c, rtk_sort_temp_bytes((int)npix, need));
-            if ((rc = ensure(c, L.d_sort_tmp, L.sort_tmp_cap, need))) return rc;
+            if ((rc = ensure(c, L.d_keys, L.keys_cap, (size_t)npix))) return rc;
+            if ((rc = ensure(c, L.d_perm, L.perm_cap, (size_t)npix))) return rc;
         }
         auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)L.d_wq[k & 1] : (rtk::QRay*)nullptr; };
-        uint32_t* cnt = L.d_wcnt;
-        dim3 fgrid = grid;
-        if (persistent) {
-            if (!c->fb_grid[mi]) {
-                int cus = 0, b1 = 0;
-                HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-                if (hw) HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (rtk_hw::first_bounce_kernel<true, true>),
-                                                                             64 * RTK_FUSED_WAVES, 0));
-                else HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (rtk_strict::first_bounce_kernel<true, true>),
-                                                                          64 * RTK_FUSED_WAVES, 0));
-                c->fb_grid[mi] = std::max(1, b1) * cus;
-            }
-            fgrid = dim3(std::min<uint32_t>((uint32_t)c->fb_grid[mi], (F.num_tiles8 + RTK_FUSED_WAVES - 1) / RTK_FUSED_WAVES));
-            F.work_counter = cnt + kRestartSlot - 1;   // last per-bounce slot, zeroed with the others
-        }
         HIPC(c, hipEventRecord(E.e[2], s));
         {
             rtk::WQ W{};
-            W.out = qbuf(1);
+            W.out = depth > 1 ? qbuf(1) : nullptr;
             W.out_count = cnt + 8 * 1 + 0;
             W.bounce = 0;
-            // <FASTONLY, NEXT>: NEXT parks the next bounce's ray (depth > 1); a depth-1 frame's
-            // fast kernel holds the top of the BVH in LDS instead
-#define RTK_FB(NS, FAST, NEXT) hipLaunchKernelGGL((NS::first_bounce_kernel<FAST, NEXT>), fgrid, block, 0, s, S, F, O, W, ax)
-            const bool nx = depth > 1;
-            if (fast_kernel) {
-                if (hw) { if (nx) RTK_FB(rtk_hw, true, true); else RTK_FB(rtk_hw, true, false); }
-                else { if (nx) RTK_FB(rtk_strict, true, true); else RTK_FB(rtk_strict, true, false); }
-            } else if (hw) {
-                RTK_FB(rtk_hw, false, true);
-            } else {
-                RTK_FB(rtk_strict, false, true);
-            }
-#undef RTK_FB
+            void* args[] = {&S, &F, &O, &W, &ax};
+            HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
         }
         HIPC(c, hipEventRecord(E.e[3], s));
         E.has_k = true;
+        // the bounce launches take no part in the adaptive order or the counter clearing
+        rtk::Frame Fb = F;
+        Fb.tile_cost = nullptr;
+        Fb.nzero = 0;
         for (int k = 1; k < depth; ++k) {  // bounce k over its queue
             rtk::WQ W{};
             W.in = qbuf(k);
             W.in_count = cnt + 8 * k + 0;
             W.perm = nullptr;
-            if (sort && RTK_COUNT_SORT) {
+            if (sort) {
                 uint32_t* hist = cnt + kSortSlot + 512 * (size_t)k;   // zeroed with the frame's counters
-                hipLaunchKernelGGL(rtk_strict::wf_hist_kernel, dim3(1024), dim3(256), 0, s, (const rtk::QRay*)qbuf(k),
+                hipLaunchKernelGGL(rtk::wf_hist_kernel, dim3(1024), dim3(256), 0, s, (const rtk::QRay*)qbuf(k),
                                    (const uint32_t*)(cnt + 8 * k + 0), (const uint32_t*)c->d_rank, c->rank_shift,
-                                   (uint8_t*)L.d_sort[0], hist);
-                hipLaunchKernelGGL(rtk_strict::wf_scatter_kernel, dim3(1024), dim3(256), 0, s,
-                                   (const uint32_t*)(cnt + 8 * k + 0), (const uint8_t*)L.d_sort[0],
-                                   (const uint32_t*)hist, hist + 256, L.d_sort[3]);
-                W.perm = L.d_sort[3];
-            } else if (sort) {
-                hipLaunchKernelGGL(rtk_strict::wf_key_kernel, dim3(1024), dim3(256), 0, s,
-                                   (const rtk::QRay*)qbuf(k), cnt + 8 * k + 0, (uint32_t)npix, L.d_sort[0],
-                                   L.d_sort[1], c->d_rank, c->rank_shift);
-                HIPC(c, rtk_sort_pairs(L.d_sort_tmp, L.sort_tmp_cap, L.d_sort[0], L.d_sort[2], L.d_sort[1],
-                                       L.d_sort[3], (int)npix, s));
-                W.perm = L.d_sort[3];
+                                   L.d_keys, hist);
+                hipLaunchKernelGGL(rtk::wf_scatter_kernel, dim3(1024), dim3(256), 0, s,
+                                   (const uint32_t*)(cnt + 8 * k + 0), (const uint8_t*)L.d_keys,
+                                   (const uint32_t*)hist, hist + 256, L.d_perm);
+                W.perm = L.d_perm;
             }
-            W.out = qbuf(k + 1);
+            W.out = k + 1 < depth ? qbuf(k + 1) : nullptr;
             W.out_count = cnt + 8 * (k + 1) + 0;
             W.fetch = cnt + 8 * k + 2;
             W.bounce = k;
-            const dim3 pg(c->wf_grid[mi]);
-            if (fast_kernel) {
-                if (hw) hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
-                else hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<true>, pg, dim3(256), 0, s, S, F, O, W, ax);
-            } else if (hw) {
-                hipLaunchKernelGGL(rtk_hw::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
-            } else {
-                hipLaunchKernelGGL(rtk_strict::wf_bounce_kernel<false>, pg, dim3(256), 0, s, S, F, O, W, ax);
-            }
-        }
-        HIPC(c, hipGetLastError());
-        HIPC(c, hipEventRecord(E.e[1], s));
-    }
-#if RTK_WAVE_TIMES
-    if (O.wave_times) {
-        HIPC(c, hipStreamSynchronize(s));
-        std::vector<uint32_t> wt((size_t)npix * 4);
-        HIPC(c, hipMemcpy(wt.data(), O.wave_times, wt.size() * 4, hipMemcpyDeviceToHost));
-        if (FILE* f = std::fopen(std::getenv("RTAMD_WAVE_TIMES"), "wb")) {
-            std::fwrite(wt.data(), 4, wt.size(), f);
-            std::fclose(f);
+            void* args[] = {&S, &Fb, &O, &W, &ax};
+            HIPC(c, hipLaunchKernel(kernel_bounce(math, fast), dim3(c->wf_grid[math]), dim3(256), args, 0, s));
         }
     }
-#endif
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipEventRecord(E.e[1], s));
+    HIPC(c, hipEventRecord(L.idle, s));
+    if (F.tile_cost) L.cost_ready = true;
+    ++L.nframe;
     c->timing_valid = true;
     ++c->frames;
     return RT_OK;
@@ -1070,9 +1069,11 @@ int rt_timing_average(rt_ctx* c, int32_t n, float* total_ms, float* traverse_ms)
 int rt_last_deferred(rt_ctx* c, uint32_t* count) {
     if (!c || !count) return RT_ERR_INVALID_ARG;
     *count = 0;
-    if (!c->last_slot || !c->last_slot->d_wcnt) return RT_OK;
-    HIPC(c, hipStreamSynchronize((hipStream_t)c->last_slot->stream));
-    HIPC(c, hipMemcpy(count, c->last_slot->d_wcnt + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    rt_ctx::FrameSlot* L = c->last_slot;
+    if (!L || !L->d_wcnt || L->nframe == 0) return RT_OK;
+    HIPC(c, hipEventSynchronize(L->idle));
+    const uint64_t par = (L->nframe - 1) & 1u;   // the last frame's parity set
+    HIPC(c, hipMemcpy(count, L->d_wcnt + par * kCounters + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

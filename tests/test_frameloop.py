@@ -40,33 +40,68 @@ def test_camera_orbit_matches_repeated_add_rotate():
     assert np.array_equal(rtamd.params_to_array(c2.params(m, 64, 48)), single)
 
 
-@pytest.mark.gpu
-def test_frames_match_the_render_abi(tmp_path):
-    import rtamd
-    w, h, depth, frames, dx, dy = 96, 64, 3, 5, 7.0, -3.0
+def _run_tool(tmp_path, w, h, depth, frames, dx, dy, flags):
     r = subprocess.run([TOOL, "--scene", "cornell", "--width", str(w), "--height", str(h), "--depth", str(depth),
                         "--frames", str(frames), "--drag", str(dx), str(dy), "--ppm-dir", str(tmp_path),
-                        "--ppm-every", "2", "--bvh-cache", str(tmp_path / "bvh.cache")],
+                        "--ppm-every", "2", "--bvh-cache", str(tmp_path / "bvh.cache"), "--flags", str(flags)],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["frames"] == frames and summary["fps"] > 0
+
+
+def _orbit_params(m, w, h, frames, dx, dy):
+    """The tool's camera per frame (rtamd.Camera = Camera.cpp + updateCamera)."""
+    import rtamd
+    cam = rtamd.Camera()
+    out = []
+    for f in range(frames):
+        if f > 0:
+            cam.add_rotate(dx * 0.25 / 100.0, dy * 0.25 / 100.0)
+        out.append(rtamd.params_to_array(cam.params(m, w, h)))
+    return out
+
+
+def _rgb(px, w, h):
+    px = px.reshape(h, w)
+    return np.stack([px & 0xFF, (px >> 8) & 0xFF, (px >> 16) & 0xFF], -1).astype(np.uint8)
+
+
+@pytest.mark.gpu
+def test_frames_match_the_oracle(tmp_path):
+    """Frames of the orbiting camera, rendered by the tool in S_strict arithmetic
+    (--flags 64), equal the CPU oracle's frames for the same camera."""
+    import rtamd
+    from oracle import oracle
+    w, h, depth, frames, dx, dy = 96, 64, 3, 5, 7.0, -3.0
+    _run_tool(tmp_path, w, h, depth, frames, dx, dy, rtamd.RT_FLAG_STRICT_MATH)
+    m = rtamd.Mesh.cornell()
+    scene = rtamd.Scene.from_mesh(m, m.build_sbvh())
+    for f, p in enumerate(_orbit_params(m, w, h, frames, dx, dy)):
+        if f % 2:
+            continue
+        ref = oracle.render(scene, p, w, h, depth=depth, aux=False)["out"]
+        assert np.array_equal(_read_ppm(tmp_path / f"frame_{f:05d}.ppm"), _rgb(ref, w, h)), f"frame {f}"
+
+
+@pytest.mark.gpu
+def test_frames_match_the_render_abi(tmp_path):
+    """Default arithmetic (S_ref): the tool's frames equal rt_render's for the same camera;
+    a second run reuses the BVH cache."""
+    import rtamd
+    w, h, depth, frames, dx, dy = 96, 64, 3, 5, 7.0, -3.0
+    _run_tool(tmp_path, w, h, depth, frames, dx, dy, 0)
     m = rtamd.Mesh.cornell()
     scene = rtamd.Scene.from_mesh(m, m.build_sbvh())
     ren = rtamd.Renderer(0)
     ren.upload(scene)
-    cam = rtamd.Camera()
-    for f in range(frames):
-        if f > 0:
-            cam.add_rotate(dx * 0.25 / 100.0, dy * 0.25 / 100.0)
+    for f, p in enumerate(_orbit_params(m, w, h, frames, dx, dy)):
         if f % 2:
             continue
-        ren.set_params(rtamd.params_to_array(cam.params(m, w, h)))
-        px = ren.render(w, h, depth=depth).reshape(h, w)
-        rgb = np.stack([px & 0xFF, (px >> 8) & 0xFF, (px >> 16) & 0xFF], -1).astype(np.uint8)
-        assert np.array_equal(_read_ppm(tmp_path / f"frame_{f:05d}.ppm"), rgb), f"frame {f}"
+        ren.set_params(p)
+        px = ren.render(w, h, depth=depth)
+        assert np.array_equal(_read_ppm(tmp_path / f"frame_{f:05d}.ppm"), _rgb(px, w, h)), f"frame {f}"
     ren.close()
-    # second run reuses the BVH cache
     r2 = subprocess.run([TOOL, "--scene", "cornell", "--width", str(w), "--height", str(h), "--frames", "2",
                          "--bvh-cache", str(tmp_path / "bvh.cache")], capture_output=True, text=True, timeout=300)
     assert r2.returncode == 0 and json.loads(r2.stdout.strip().splitlines()[-1])["bvh_cached"] is True

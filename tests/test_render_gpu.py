@@ -1,9 +1,13 @@
 """Parity of the HIP render path (through the C ABI) with the CPU oracle.
 
-Bar: hit ids bit-exact, closest-hit t and float RGB bit-exact
-(the north star allows 1e-4 on RGB; the S_strict semantics make both sides
-deterministic so the test demands identity and reports the 1e-4 check
-separately), packed pixels bit-exact.
+The oracle computes S_strict arithmetic, so every comparison with it
+renders with RT_FLAG_STRICT_MATH.  Bar: hit ids bit-exact, closest-hit
+t and float RGB bit-exact (the north star allows 1e-4 on RGB; the S_strict semantics
+make both sides deterministic so the test demands identity and reports the 1e-4
+check separately), packed pixels bit-exact.  The default arithmetic (S_ref, the
+reference's own build) is pinned to the reference kernel in test_reference_pin_gpu.py;
+GPU-vs-GPU comparisons here (tilings, streams, fused vs wavefront, fast vs division
+slab test) run in the default mode or in all three.
 """
 import numpy as np
 import pytest
@@ -13,6 +17,8 @@ from conftest import golden_names, load_golden
 pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-4  # north star tolerance on float RGB
+STRICT = 64      # RT_FLAG_STRICT_MATH: the oracle's arithmetic
+MODES = {"ref": 0, "strict": STRICT, "hw": 2}   # default S_ref, S_strict, S_hw (RT_FLAG_HW_MATH)
 
 
 def _scene(d):
@@ -42,9 +48,9 @@ def test_fixture_depth3(renderer, name):
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     w, h = int(d["w"]), int(d["h"])
-    gpu = renderer.render(w, h, depth=3, aux=True)
+    gpu = renderer.render(w, h, depth=3, flags=STRICT, aux=True)
     _compare(gpu, _oracle(d, 3), name)
-    plain = renderer.render(w, h, depth=3)
+    plain = renderer.render(w, h, depth=3, flags=STRICT)
     assert np.array_equal(plain, gpu["out"])
 
 
@@ -55,7 +61,7 @@ def test_depth_and_flags(renderer, name, depth, flags):
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     w, h = int(d["w"]), int(d["h"])
-    gpu = renderer.render(w, h, depth=depth, flags=flags, aux=True)
+    gpu = renderer.render(w, h, depth=depth, flags=flags | STRICT, aux=True)
     ref = _oracle(d, depth, flags)
     _compare(gpu, ref, f"{name} depth={depth} flags={flags}")
 
@@ -68,7 +74,7 @@ def test_odd_sizes(renderer):
         m = rtamd.Mesh.torus_knot(128, 64)
         p = rtamd.params_to_array(m.camera_params(w, h))
         renderer.set_params(p)
-        gpu = renderer.render(w, h, depth=3, aux=True)
+        gpu = renderer.render(w, h, depth=3, flags=STRICT, aux=True)
         _compare(gpu, _oracle(d, 3, w=w, h=h, params=p), f"{w}x{h}")
 
 
@@ -81,9 +87,9 @@ def test_render_into_pinned_and_pageable_host_memory(renderer):
     w, h = int(d["w"]), int(d["h"])
     ref = _oracle(d, 1)["out"]
     pageable = np.zeros(w * h, np.uint32)
-    renderer.render_host_ptr(w, h, 1, 0, pageable.ctypes.data)
+    renderer.render_host_ptr(w, h, 1, STRICT, pageable.ctypes.data)
     pinned = torch.zeros(w * h, dtype=torch.int32, pin_memory=True)
-    renderer.render_host_ptr(w, h, 1, 0, pinned.data_ptr())
+    renderer.render_host_ptr(w, h, 1, STRICT, pinned.data_ptr())
     assert np.array_equal(pageable, ref)
     assert np.array_equal(pinned.numpy().view(np.uint32), ref)
     with pytest.raises(ValueError):
@@ -95,7 +101,7 @@ def test_overflow_counter(renderer):
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     before = renderer.overflow_count()
-    gpu = renderer.render(int(d["w"]), int(d["h"]), depth=3, aux=True)
+    gpu = renderer.render(int(d["w"]), int(d["h"]), depth=3, flags=STRICT, aux=True)
     ref = _oracle(d, 3)
     _compare(gpu, ref, "overflow_comb")
     assert ref["stats"]["stack_overflow"] > 0
@@ -212,17 +218,19 @@ def test_errors(renderer):
     r.close()
 
 
+@pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("name", ["hf40k", "knot16k", "cubes2_obj", "rand3k_bigleaf"])
-def test_fast_division_is_bit_identical(renderer, name):
-    """The 3-op slab quotient against the IEEE-division slab test."""
+def test_fast_division_is_bit_identical(renderer, name, mode):
+    """The fast slab quotient (Markstein's 3 ops in S_strict / S_hw, one
+    multiply by the 2.5-ulp reciprocal in S_ref) against the mode's division form."""
     import rtamd
     d = load_golden(name)
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     w, h = int(d["w"]), int(d["h"])
-    fast = renderer.render(w, h, depth=3, aux=True)
-    slow = renderer.render(w, h, depth=3, flags=rtamd.RT_FLAG_EXACT_DIV, aux=True)
-    _compare(fast, slow, name + " fast-vs-exact division")
+    fast = renderer.render(w, h, depth=3, flags=MODES[mode], aux=True)
+    slow = renderer.render(w, h, depth=3, flags=MODES[mode] | rtamd.RT_FLAG_EXACT_DIV, aux=True)
+    _compare(fast, slow, f"{name} {mode} fast-vs-division")
 
 
 def test_tiny_coordinates_fall_back_to_division(renderer):
@@ -235,10 +243,14 @@ def test_tiny_coordinates_fall_back_to_division(renderer):
     p = rtamd.params_to_array(m.camera_params(64, 64))
     renderer.upload(s)
     renderer.set_params(p)
-    gpu = renderer.render(64, 64, depth=3, aux=True)
+    gpu = renderer.render(64, 64, depth=3, flags=STRICT, aux=True)
     from oracle import oracle
     ref = oracle.render(s, p, 64, 64, depth=3)
     _compare(gpu, ref, "tiny coordinates")
+    for mode in ("ref", "hw"):   # the division form is the only one that runs here
+        fast = renderer.render(64, 64, depth=3, flags=MODES[mode], aux=True)
+        slow = renderer.render(64, 64, depth=3, flags=MODES[mode] | rtamd.RT_FLAG_EXACT_DIV, aux=True)
+        _compare(fast, slow, "tiny coordinates " + mode)
 
 
 def test_zero_direction_component_pixels(renderer):
@@ -263,9 +275,32 @@ def test_zero_direction_component_pixels(renderer):
     p[7, :3] = d["scene_max"]
     p = p.reshape(-1)
     renderer.set_params(p)
-    gpu = renderer.render(w, h, depth=3, aux=True)
+    gpu = renderer.render(w, h, depth=3, flags=STRICT, aux=True)
     _compare(gpu, _oracle(d, 3, w=w, h=h, params=p), "axis-aligned camera")
     assert renderer.last_deferred() == 0
+    import rtamd
+    for mode in ("ref", "hw"):   # zero components through each mode's fast quotient
+        fast = renderer.render(w, h, depth=3, flags=MODES[mode], aux=True)
+        slow = renderer.render(w, h, depth=3, flags=MODES[mode] | rtamd.RT_FLAG_EXACT_DIV, aux=True)
+        _compare(fast, slow, "axis-aligned camera " + mode)
+
+
+@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("depth", [1, 3])
+@pytest.mark.parametrize("sort", [False, True])
+def test_wavefront_path_matches_oracle(renderer, name, depth, sort):
+    """RT_FLAG_WAVEFRONT (one launch per bounce over a compacted ray queue, optionally
+    sorted per bounce) against the CPU oracle directly, aux planes included."""
+    import rtamd
+    d = load_golden(name)
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    flags = STRICT | rtamd.RT_FLAG_WAVEFRONT | (rtamd.RT_FLAG_WF_SORT if sort else 0)
+    ref = _oracle(d, depth)
+    _compare(renderer.render(w, h, depth=depth, flags=flags, aux=True), ref, f"{name} depth={depth} sort={sort}")
+    # second frame: longest-first block order from the first one's times
+    _compare(renderer.render(w, h, depth=depth, flags=flags, aux=True), ref, f"{name} depth={depth} sort={sort} (2)")
 
 
 @pytest.mark.parametrize("name", golden_names())
@@ -296,9 +331,9 @@ def test_adaptive_block_order_is_bit_identical(renderer, name):
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     w, h = int(d["w"]), int(d["h"])
-    static = renderer.render(w, h, depth=3, flags=rtamd.RT_FLAG_STATIC_ORDER, aux=True)
-    first = renderer.render(w, h, depth=3, aux=True)   # measures
-    second = renderer.render(w, h, depth=3, aux=True)  # longest-first order
+    static = renderer.render(w, h, depth=3, flags=rtamd.RT_FLAG_STATIC_ORDER | STRICT, aux=True)
+    first = renderer.render(w, h, depth=3, flags=STRICT, aux=True)   # measures
+    second = renderer.render(w, h, depth=3, flags=STRICT, aux=True)  # longest-first order
     _compare(first, static, name + " first adaptive frame")
     _compare(second, static, name + " adaptive order")
     _compare(second, _oracle(d, 3), name + " adaptive vs oracle")
@@ -315,5 +350,5 @@ def test_sbvh_scene_parity(renderer, make):
     p = rtamd.params_to_array(m.camera_params(w, h))
     renderer.upload(s)
     renderer.set_params(p)
-    gpu = renderer.render(w, h, depth=3, aux=True)
+    gpu = renderer.render(w, h, depth=3, flags=STRICT, aux=True)
     _compare(gpu, oracle.render(s, p, w, h, depth=3), "sbvh " + make)
