@@ -5,18 +5,22 @@ One step = one frame: every rank renders its screen bands of the 1080p frame
 gathered to rank 0 over RCCL and re-interleaved into the frame.
 `value` = rays traced by all ranks (primary + shadow) / max-over-ranks time.
 
-    python bench.py [--gpus N --steps K --warmup W --config c3]
+    python bench.py [--gpus N --steps K --warmup W --config c3 --orbit 0.01]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+`--gpus N` without a torch.distributed environment starts torch.distributed.run with N
+ranks as a child process (before anything touches the GPU) and passes rank 0's JSON
+line through; under torchrun, WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "real-time-opencl-raytracer_amd")
@@ -24,81 +28,27 @@ for _p in (PKG, ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-# Frames in flight run on separate streams; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
-# queues (4 by default, and exported as 4 on the GPU boxes; shared with torch's and the
-# library's own streams), so with four frames in flight two would share a queue and
-# serialise.  Raised to at least 8, before HIP starts (measured: 1/8 shard 0.075 -> 0.055 ms).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
 METRIC = "Mrays/sec (primary+1 shadow) @1080p, 1M-tri SAH BVH; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# C3 terrain extent: fills the default camera's 1080p view (Camera.cpp:6-19)
-HF_EXT = (-150.0, 650.0, -150.0, 650.0)
-
-CONFIGS = {
-    # BASELINE.json configs[2] -- the metric's configuration
-    "c3": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=HF_EXT, w=1920, h=1080, depth=1, flags=0,
-               desc="C3: 1M-tri value-noise heightfield (500x1000 cells x2, seed 0x5EED), 1920x1080, "
-                    "primary + 1 shadow ray"),
-    # configs[1]: ~70k-tri mesh, primary only
-    "c2": dict(scene="knot", nu=256, nv=137, w=1920, h=1080, depth=1, flags=1,
-               desc="C2: 70,144-tri torus knot, 1920x1080, primary rays only"),
-    # configs[3]: C3 scene at 4K (multi-GPU scaling curve)
-    "c4": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=HF_EXT, w=3840, h=2160, depth=1, flags=0,
-               desc="C4: C3 scene at 3840x2160, primary + 1 shadow ray"),
-    # configs[4]: 10M tris (10 x C3 on a 5x2 grid), depth 3 (primary + 2 bounces, shadows), in
-    # the wavefront mode with per-bounce ray sorting, as the config names it: flags 8 | 32 =
-    # RT_FLAG_WAVEFRONT | RT_FLAG_WF_SORT
-    "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920, h=1080, depth=3,
-               flags=8 | 32,
-               dae=False,  # a 1 GB Collada text file is not worth the round trip; built in memory
-               desc="C5: 10M-tri merged scene (10 x C3 on a 5x2 grid), 1920x1080, 3 bounces with shadows, "
-                    "wavefront mode with per-bounce ray sorting"),
-    # the same without the sort: faster here, the sort costs more than the coherence it buys;
-    # with frames in flight the per-bounce launches also beat the fused kernel
-    "c5u": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920, h=1080, depth=3,
-                flags=8, dae=False,
-                desc="C5 scene and frame, wavefront mode without ray sorting"),
-}
+MATH = {0: "S_ref: the reference kernel as RayTracer.cpp builds it (bit-exact vs its gfx950 build)",
+        64: "S_strict: the CPU oracle's arithmetic (RT_FLAG_STRICT_MATH)",
+        2: "S_hw: the reference built with IEEE / and sqrt (RT_FLAG_HW_MATH)"}
 
 
-def make_scene(cfg, threads, builder="sbvh", via_dae=True):
-    """The config's synthetic mesh; with via_dae (configs C2-C4) it is written
-    as the reference-subset Collada file and read back through the ColladaLoader path
-    (rt_mesh_save_dae / rt_mesh_load_dae), as the reference application loads its scene."""
-    import tempfile
-    import rtamd
-    if cfg["scene"] == "heightfield":
-        mesh = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"], cfg["ext"])
-    elif cfg["scene"] == "knot":
-        mesh = rtamd.Mesh.torus_knot(cfg["nu"], cfg["nv"])
-    elif cfg["scene"] == "hf10":
-        tile = rtamd.Mesh.heightfield(cfg["nx"], cfg["nz"], cfg["amp"], cfg["seed"], cfg["ext"])
-        mesh = rtamd.Mesh()
-        mesh.append_grid(tile, 5, 2, 160.0, 400.0, 1.0)
-    else:
-        raise ValueError(cfg["scene"])
-    if via_dae and cfg.get("dae", True):
-        with tempfile.TemporaryDirectory() as td:
-            path = os.path.join(td, "scene.dae")
-            mesh.save_dae(path)
-            mesh = rtamd.Mesh.load_dae(path)
-    t0 = time.time()
-    bvh = mesh.build_sbvh(threads) if builder == "sbvh" else mesh.build_bvh(8, threads)
-    return mesh, bvh, time.time() - t0
-
-
-def main():
+def parse_args(argv=None):
+    from rtamd.configs import CONFIGS
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)   # 0.2 s of frames: steady state, not clock ramp-up
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--orbit", type=float, default=0.0,
+                    help="moving camera: add_rotate(ORBIT, 0) radians per frame, as the reference's mouse "
+                         "drag does (RayTracer.cpp:553-565); 0 = the static default camera")
     ap.add_argument("--band-rows", type=int, default=8,
                     help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
     ap.add_argument("--dist", action="store_true", help="use the process-group gather path even at N = 1")
-    ap.add_argument("--gather", default="native", choices=["torch", "native"],
+    ap.add_argument("--gather", default="torch", choices=["torch", "native"],
                     help="band exchange at N > 1: torch.distributed gather (async, RCCL) + rt_assemble_bands, or "
                          "the library's own RCCL communicators on the frame's stream (rt_frame_gather)")
     ap.add_argument("--inflight", type=int, default=4,
@@ -109,15 +59,79 @@ def main():
                     help="sbvh: the reference's SplitBVHBuilder (same bytes); binned: binned-SAH object splits")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--extra-flags", type=int, default=0, help="OR-ed into rt_render flags (A/B: 2 = HW math, "
-                    "4 = IEEE-division slab test)")
-    args = ap.parse_args()
+    ap.add_argument("--extra-flags", type=int, default=0,
+                    help="OR-ed into rt_render flags (A/B: 64 = S_strict math, 2 = S_hw math, 4 = division-form "
+                         "slab test, 16 = static block order)")
+    ap.add_argument("--probe-launch", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group and rank 0 reports the world")
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(n: int, argv, port: int):
+    """torch.distributed.run with n ranks of this script on one node (the driver's form)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def _probe(args):
+    """--probe-launch: the rendezvous of the launched ranks, with gloo on the CPU."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    ranks = [None] * world
+    dist.all_gather_object(ranks, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "all_reduce": float(t.item()),
+                          "ranks": ranks}))
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # N ranks requested from a plain `python bench.py --gpus N`: one process per GPU via
+        # torch.distributed.run, started before this process touches the GPU
+        rc = subprocess.call(launcher_cmd(args.gpus, sys.argv[1:], _free_port()),
+                             env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+        sys.exit(rc)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: the ranks must be the GPUs asked for")
+    if args.probe_launch:
+        _probe(args)
+        return
+    run(args, world)
+
+
+def run(args, world):
+    # Frames in flight run on separate streams; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
+    # queues (4 by default, and exported as 4 on the GPU boxes; shared with torch's and the
+    # library's own streams), so with four frames in flight two would share a queue and
+    # serialise.  Raised to at least 8 before HIP starts (measured: 1/8 shard 0.075 -> 0.055 ms).
+    # Under rocprofv3 the profiler's preload starts HIP first, so the profiling scripts set it
+    # in their own environment; the JSON says which applied.
+    q_in = os.environ.get("GPU_MAX_HW_QUEUES")
+    hw_queues = {"value": int(q_in) if q_in else 4, "source": "inherited" if q_in else "HIP default"}
+    if hw_queues["value"] < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+        hw_queues = {"value": 8, "source": "set by bench.py (was %s)" % (q_in or "unset")}
+
+    import numpy as np
     import torch
     import torch.distributed as dist
     import rtamd
+    from rtamd import configs
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
@@ -126,26 +140,61 @@ def main():
     # --dist: the distributed frame path (process group, gather, assembly) even at N = 1,
     # to exercise it on a one-GPU box
     use_dist = world > 1 or args.dist
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    cfg = CONFIGS[args.config]
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = configs.CONFIGS[args.config]
     w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"] | args.extra_flags
+    math_flags = flags & (64 | 2)
+    host_threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    nframes = args.warmup + args.steps
 
-    host_threads = max(1, min(16, (os.cpu_count() or 1)) // max(1, world))
-    mesh, bvh, build_s = make_scene(cfg, host_threads, args.bvh, not args.direct)
-    scene = rtamd.Scene.from_mesh(mesh, bvh)
-    params = rtamd.params_to_array(mesh.camera_params(w, h))
+    # ---- scene: rank 0 builds it (Collada round trip + the reference's SBVH) and uploads it;
+    # at N > 1 its device image is broadcast over RCCL and every other rank loads it ----
     r = rtamd.Renderer(local)
-    r.upload(scene)
-    r.set_params(params)
+    mesh = bvh = None
+    build_s = 0.0
+    t_scene = time.perf_counter()
+    if rank == 0:
+        mesh, bvh, build_s = configs.make_scene(cfg, host_threads, args.bvh, not args.direct)
+        r.upload(rtamd.Scene.from_mesh(mesh, bvh))
+        if args.orbit:
+            cam = rtamd.Camera()
+            plist = []
+            for f in range(nframes):
+                if f > 0:
+                    cam.add_rotate(args.orbit, 0.0)
+                plist.append(rtamd.params_to_array(cam.params(mesh, w, h)))
+            ptab = np.stack(plist)
+        else:
+            ptab = rtamd.params_to_array(mesh.camera_params(w, h))[None, :]
+    scene_bytes = 0
+    if world > 1:
+        nb = torch.zeros(2, dtype=torch.int64, device=dev)
+        if rank == 0:
+            nb[0] = r.scene_image_size()
+            nb[1] = ptab.shape[0]
+        dist.broadcast(nb, src=0)
+        scene_bytes = int(nb[0].item())
+        img = torch.empty(scene_bytes, dtype=torch.uint8, device=dev)
+        pt = torch.empty((int(nb[1].item()), 32), dtype=torch.float32, device=dev)
+        if rank == 0:
+            r.pack_scene(img.data_ptr(), scene_bytes, torch.cuda.current_stream().cuda_stream)
+            pt.copy_(torch.from_numpy(ptab))
+        dist.broadcast(img, src=0)
+        dist.broadcast(pt, src=0)
+        if rank != 0:
+            torch.cuda.synchronize(dev)
+            r.load_scene(img.data_ptr(), scene_bytes)
+            ptab = pt.cpu().numpy()
+        del img, pt
+    scene_s = time.perf_counter() - t_scene
+    r.set_params(ptab[0])
 
     # --shard R/N (diagnostic, world 1 only): render just shard R of an N-way band split,
     # i.e. one rank's kernel work at N GPUs without the gather
@@ -175,18 +224,21 @@ def main():
     frames = [torch.zeros(h * w, dtype=torch.int32, device=dev) for _ in range(F)] \
         if (rank == 0 and use_dist) else None
 
-    # rays traced per frame by this rank (counted once with the aux planes)
+    # rays traced by this rank in a frame with params p (counted with the aux planes, untimed)
     d = max(depth, 1)
     hits = torch.zeros(npx * d * 2, dtype=torch.int32, device=dev)
     tt = torch.zeros(npx * d, dtype=torch.float32, device=dev)
     rgb = torch.zeros(npx * 3, dtype=torch.float32, device=dev)
-    r.render_device(w, h, depth, flags, outs[0].data_ptr(), tiling=tiling, stream=streams[0].cuda_stream,
-                    aux_ptrs=(hits.data_ptr(), tt.data_ptr(), rgb.data_ptr()))
-    torch.cuda.synchronize(dev)
-    hv = hits.view(npx, d, 2)
-    rays_local = int((hv[..., 0] != -2).sum().item()) + int((hv[..., 1] != -2).sum().item())
-    prim_local = int((hv[:, 0, 0] != -2).sum().item())
-    del hits, tt, rgb
+
+    def count_rays(p):
+        r.set_params(p)
+        r.render_device(w, h, depth, flags, outs[0].data_ptr(), tiling=tiling, stream=streams[0].cuda_stream,
+                        aux_ptrs=(hits.data_ptr(), tt.data_ptr(), rgb.data_ptr()))
+        torch.cuda.synchronize(dev)
+        hv = hits.view(npx, d, 2)
+        return int((hv != -2).sum().item()), int((hv[:, 0, 0] != -2).sum().item())
+
+    rays_f0, prim_f0 = count_rays(ptab[0])
 
     # One step = one frame: render this rank's bands -> (N > 1) async RCCL gather of the bands
     # to rank 0 -> rank 0 re-interleaves them into the frame.  A slot's previous frame is
@@ -194,10 +246,13 @@ def main():
     pending = [None] * F
     nstep = [0]
     # the per-frame host path, with everything constant bound once: at N = 8 a frame is
-    # ~0.055 ms of GPU time, so the host's enqueue per frame has to stay well under that
+    # ~0.05 ms of GPU time, so the host's enqueue per frame has to stay well under that
     launch = r.frame_launcher(w, h, depth, flags, tiling)
     sh = [st.cuda_stream for st in streams]
     out_ptr = [o.data_ptr() for o in outs]
+    orbit_params = [rtamd.array_to_params(p) for p in ptab] if args.orbit else None
+    set_params = rtamd.lib().rt_set_params
+    hdl = r._h
     if use_dist:
         pg = dist.distributed_c10d._get_default_group()
         gopts = dist.GatherOptions()
@@ -251,11 +306,14 @@ def main():
             assemble(frame_ptr[k], gbuf_ptr[k], sh[k])
 
     def step():
-        k = nstep[0] % F
+        n = nstep[0]
+        k = n % F
         nstep[0] += 1
         torch.cuda.set_stream(streams[k])
         if pending[k] is not None:
             finish(k)
+        if orbit_params is not None:   # updateCamera (RayTracer.cpp:609-672) for this frame
+            set_params(hdl, orbit_params[n])
         launch(out_ptr[k], sh[k])
         if native:     # gather + assembly on the frame's own stream: no cross-stream waits
             comms[k].frame_gather(out_ptr[k], cap, slots_ptr[k], fr_ptr[k], w, h, args.band_rows, sh[k])
@@ -288,17 +346,29 @@ def main():
     elapsed = time.perf_counter() - t0
     torch.cuda.set_stream(streams[0])
 
+    # per-launch kernel times of the timed steps, from the HIP events the library
+    # records on the launch stream around each frame's kernels (ring of 64 frames)
+    frame_ms_avg, kernel_ms_avg = r.timing_average(min(args.steps, 64))
+
+    # rays of the timed frames (untimed: one aux render per distinct camera)
+    if args.orbit:
+        rays_local = prim_local = 0
+        for p in ptab[args.warmup:]:
+            a, b = count_rays(p)
+            rays_local += a
+            prim_local += b
+        r.set_params(ptab[0])
+    else:
+        rays_local, prim_local = rays_f0 * args.steps, prim_f0 * args.steps
+    del hits, tt, rgb
+
     # check (untimed): rank 0's assembled frames equal its own one-rank render of the frame
     frame_ok = None
-    if use_dist and rank == 0:
+    if use_dist and rank == 0 and not args.orbit:
         full = torch.zeros(h * w, dtype=torch.int32, device=dev)
         r.render_device(w, h, depth, flags, full.data_ptr(), stream=streams[0].cuda_stream)
         torch.cuda.synchronize(dev)
         frame_ok = all(bool(torch.equal(full, f)) for f in frames)
-
-    # per-launch kernel times of the timed steps, from the HIP events the library
-    # records on the launch stream around each frame's kernels (ring of 64 frames)
-    frame_ms_avg, kernel_ms_avg = r.timing_average(min(args.steps, 64))
 
     # (untimed for `value`) the reference's own boundary: rt_render, synchronous, the frame
     # read back into host memory (raytrace_gpgpu: launch + clFinish + clEnqueueReadBuffer,
@@ -317,7 +387,7 @@ def main():
         ms_pin = host_rate(pinned.data_ptr())
         host_boundary = {"api": "rt_render (synchronous, frame copied to host memory)",
                          "ms_per_frame_pageable": round(ms_pg, 4), "ms_per_frame_pinned": round(ms_pin, 4),
-                         "mrays_per_s_pinned": round(rays_local / (ms_pin * 1e-3) / 1e6, 1)}
+                         "mrays_per_s_pinned": round(rays_f0 / (ms_pin * 1e-3) / 1e6, 1)}
 
     if use_dist:
         t = torch.tensor([elapsed, float(rays_local), float(prim_local)], dtype=torch.float64, device=dev)
@@ -334,7 +404,7 @@ def main():
         rays_total, prim_total = float(rays_local), float(prim_local)
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = rays_total * args.steps / elapsed / 1e6
+    value = rays_total / elapsed / 1e6
 
     if rank != 0:
         if world > 1:
@@ -344,14 +414,16 @@ def main():
             dist.destroy_process_group()
         return
 
-    # CPU oracle sample: algorithmic bytes/ray (roofline) + CPU baseline
+    # ---- CPU oracle leg (rank 0): algorithmic record fetches per frame (roofline), the CPU
+    # baseline, and the parity check of an S_strict GPU frame against the oracle's ----
     from oracle import oracle
+    scene = rtamd.Scene.from_mesh(mesh, bvh)
     cpu = None
-    bpr = None
+    parity = None
     budget = args.cpu_seconds if (world == 1 and not args.no_cpu_baseline) else min(args.cpu_seconds, 5.0)
-    ncores = min(16, os.cpu_count() or 1)
+    ncores = host_threads
     tprobe = time.perf_counter()
-    probe = oracle.render(scene, params, w, h, depth=depth, flags=flags, pixels=(0, (w * h) // 4093, 4093),
+    probe = oracle.render(scene, ptab[0], w, h, depth=depth, flags=flags, pixels=(0, (w * h) // 4093, 4093),
                           nthreads=ncores, aux=False)
     tprobe = time.perf_counter() - tprobe
     per_px = tprobe / max(1, (w * h) // 4093)
@@ -363,7 +435,7 @@ def main():
     t0 = time.perf_counter()
     reps = 0
     while True:
-        samp = oracle.render(scene, params, w, h, depth=depth, flags=flags, pixels=(0, npix_sample, stride),
+        samp = oracle.render(scene, ptab[0], w, h, depth=depth, flags=flags, pixels=(0, npix_sample, stride),
                              nthreads=ncores, aux=False)
         reps += 1
         cpu_s = time.perf_counter() - t0
@@ -372,12 +444,26 @@ def main():
     st = samp["stats"]
     cpu_rays = sum(st[k]["rays"] for k in ("primary", "shadow", "secondary"))
     kinds = [k for k in ("primary", "shadow", "secondary") if st[k]["rays"]]
-    tot_bytes = sum(80.0 * st[k]["inner"] + 16.0 * st[k]["leaf"] + 64.0 * st[k]["tris"] for k in kinds)
-    bpr = tot_bytes / max(1, cpu_rays)
+    # per traced ray (oracle, reference visit order): the reference layout's bytes (SURVEY.md
+    # 8d) and this layout's record fetches (one 64-B inner record per inner visit, one 48-B
+    # triangle record per triangle test; leaves cost none: their range is in the child ref)
+    bpr = sum(80.0 * st[k]["inner"] + 16.0 * st[k]["leaf"] + 64.0 * st[k]["tris"] for k in kinds) / max(1, cpu_rays)
+    rec_inner = sum(st[k]["inner"] for k in kinds) / max(1, cpu_rays)
+    rec_tri = sum(st[k]["tris"] for k in kinds) / max(1, cpu_rays)
     if world == 1 and not args.no_cpu_baseline:
         cpu = {"value": cpu_rays * reps / cpu_s / 1e6, "unit": "Mrays/s", "cores": ncores, "kind": "port",
                "sample": f"oracle/rt_oracle.c on every {stride}th pixel of the same frame ({npix_sample} px, "
-                         f"{cpu_rays} rays) x {reps} repetition(s), {cpu_s:.1f} s, {ncores} threads"}
+                         f"{cpu_rays} rays) x {reps} repetition(s), {cpu_s:.1f} s, {ncores} threads "
+                         f"(the box's CPU share; os.cpu_count() = {os.cpu_count()})"}
+        if stride == 1:
+            # the oracle's frame against the GPU's frame in the oracle's arithmetic (S_strict),
+            # whole frame, same camera; the benched arithmetic is pinned to the reference
+            # kernel itself by tests/test_fullsize_gpu.py
+            r.set_params(ptab[0])
+            gpu = r.render(w, h, depth=depth, flags=(flags & ~2) | 64)
+            parity = {"mode": "S_strict (RT_FLAG_STRICT_MATH) vs oracle/rt_oracle.c", "pixels": int(w * h),
+                      "equal": bool(np.array_equal(gpu, samp["out"])),
+                      "differing_pixels": int(np.sum(gpu != samp["out"]))}
 
     # measured device copy rate (the roofline also against a measured stream-copy
     # peak): 1 GiB -> 1 GiB device-to-device copies, read + write bytes over HIP-event time
@@ -393,23 +479,14 @@ def main():
     stream_copy_gbs = 10 * 2 * src.numel() * 4 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
     del src, dst
 
-    # algorithmic bytes per launch = rays this launch traces x bytes/ray + 4 B/pixel output
-    launch_rays = rays_total / max(1, world)
-    launch_px = (w * h) / world if world > 1 else npx
-    launch_bytes = launch_rays * bpr + 4.0 * launch_px
-    achieved = launch_bytes / (kernel_ms_avg * 1e-3) / 1e9
-    # with F frames in flight the launches overlap, so a launch's duration includes the time it
-    # shares the GPU with its neighbours: the per-launch rate above under-reads the kernel's
-    # throughput by up to ~F x.  The aggregate rate is the same bytes over the wall time per frame.
-    achieved_aggregate = launch_bytes / (ms_per_step * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(pmc_path):
-        try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    frame_rays = rays_total / args.steps
+    frame_px = float(w * h) if not args.shard else float(npx)
+    alg_bytes = frame_rays * bpr + 4.0 * frame_px            # reference-layout bytes per frame
+    records = frame_rays * (rec_inner + rec_tri)              # this layout's record fetches per frame
+    wavefront = depth > 1 and (flags & 8)
+    ns = {0: "rtk_ref", 64: "rtk_strict", 2: "rtk_hw"}[math_flags]
+    kname = (f"{ns}::first_bounce_kernel<true, {'true' if depth > 1 else 'false'}>" if (depth == 1 or wavefront)
+             else f"{ns}::render_kernel<true>")
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -425,33 +502,39 @@ def main():
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "config": args.config, "triangles": mesh.num_triangles,
                    "bvh_nodes": int(bvh.nodes.shape[0]), "width": w, "height": h, "depth": depth,
-                   "shadow": not (flags & 1), "rays_per_frame": int(rays_total),
-                   "primary_rays_per_frame": int(prim_total),
-                   "primary_mrays_per_s": round(prim_total * args.steps / elapsed / 1e6, 1),
-                   "mpixels_per_s": round(w * h * args.steps / elapsed / 1e6, 1),"parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
+                   "shadow": not (flags & 1), "math": MATH[math_flags], "flags": flags,
+                   "camera": (f"orbit: add_rotate({args.orbit}, 0) per frame (RayTracer.cpp:553-565)" if args.orbit
+                              else "static default camera (Camera.cpp:6-19)"),
+                   "block_order": "static" if flags & 16 else "adaptive longest-first from the previous frame",
+                   "rays_per_frame": round(frame_rays, 1),
+                   "primary_rays_per_frame": round(prim_total / args.steps, 1),
+                   "primary_mrays_per_s": round(prim_total / elapsed / 1e6, 1),
+                   "mpixels_per_s": round(w * h * args.steps / elapsed / 1e6, 1),
+                   "parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
                                    else f"shard {args.shard} of the band split (diagnostic, no gather)"),
                    "band_rows": args.band_rows, "frames_in_flight": F,
                    "band_exchange": (None if not use_dist else "rt_frame_gather (library RCCL communicators)" if native
                                      else "torch.distributed gather (RCCL) + rt_assemble_bands"),
-                   "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                   "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4), "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)"
-                                                        if args.bvh == "sbvh" else "binned SAH"),
+                   "scene_distribution": (f"rank 0 builds; {scene_bytes} B scene image broadcast over RCCL "
+                                          "(rt_scene_image_pack / _load)" if world > 1 else "single rank"),
+                   "scene_setup_s": round(scene_s, 3),
+                   "gpu_max_hw_queues": hw_queues,
+                   "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
+                   "bvh": ("SplitBVHBuilder (reference SBVH, same bytes)" if args.bvh == "sbvh" else "binned SAH"),
                    "bvh_refs": int(bvh.tri_indices.size), "bvh_build_s": round(build_s, 3),
                    "scene_source": "Collada (rt_mesh_load_dae)" if (cfg.get("dae", True) and not args.direct)
                    else "in-memory generator"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "achieved_aggregate": round(achieved_aggregate, 2),
-                     "frac_aggregate": round(achieved_aggregate / HBM_PEAK_GBS, 4),
-                     "stream_copy_gbs": round(stream_copy_gbs, 1),
-                     "frac_of_stream_copy": round(achieved / stream_copy_gbs, 4),
-                     "launches_overlap": F > 1,
-                     "bytes_per_ray": round(bpr, 1), "kernel_ms": round(kernel_ms_avg, 4),
-                     "frame_kernels_ms": round(frame_ms_avg, 4),
-                     "kernel": ("rtk_strict::first_bounce_kernel<true, false>" if depth == 1 else "rtk_strict::first_bounce_kernel<true, true>" if (flags & 8)
-                                else "rtk_strict::render_kernel<true>")},
+        "roofline": {"bound": "hbm", "achieved": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(alg_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_ray": round(bpr, 1), "records_per_ray": round(rec_inner + rec_tri, 2),
+                     "record_fetches_per_frame": round(records), "stream_copy_gbs": round(stream_copy_gbs, 1),
+                     "kernel_ms": round(kernel_ms_avg, 4), "frame_kernels_ms": round(frame_ms_avg, 4),
+                     "launches_overlap": F > 1, "kernel": kname},
         "cpu_baseline": cpu,
     }
+    if parity is not None:
+        res["parity_vs_oracle"] = parity
     if frame_ok is not None:
         res["config"]["gathered_frame_equals_single_rank_render"] = frame_ok
     if host_boundary is not None:

@@ -139,6 +139,19 @@ int rt_upload_scene(rt_ctx* ctx, const rt_float4* verts, int32_t nv, const int32
                     const rt_float4* normals, int32_t nnorm, const int32_t* normal_idx,
                     const rt_material* mats, int32_t nmat, const int32_t* tri_to_mat);
 
+/* Multi-GPU scene distribution ("ncclBroadcast of scene buffers at load").
+ * The reference uploads one scene to its one device (RayTracer.cpp:942-984); here one
+ * rank builds and uploads it, packs its device layouts into ONE contiguous device
+ * buffer (the "scene image"), that buffer is broadcast over RCCL, and every other rank
+ * loads it -- the Collada parse and the SBVH build run once per node, not per GPU.
+ *   rt_scene_image_size : bytes of ctx's scene image
+ *   rt_scene_image_pack : device-to-device copy of ctx's scene into d_image (synchronizes stream)
+ *   rt_scene_image_load : replace ctx's scene by the image's (synchronizes stream)
+ * The image is position-independent device data: pack on one ctx, load on any other. */
+int rt_scene_image_size(rt_ctx* ctx, uint64_t* bytes);
+int rt_scene_image_pack(rt_ctx* ctx, void* d_image, uint64_t bytes, void* stream);
+int rt_scene_image_load(rt_ctx* ctx, const void* d_image, uint64_t bytes, void* stream);
+
 /* Replaces updateCamera's clEnqueueWriteBuffer of Params (RayTracer.cpp:671). */
 int rt_set_params(rt_ctx* ctx, const rt_params* params);
 

@@ -1,6 +1,7 @@
 """Run the reference OpenCL kernel (compiled by oracle/Makefile.ref into
 oracle/_ref/) on the GPU.  TEST INFRASTRUCTURE ONLY: used to pin the oracle
-(tests/golden/make_golden.py, tests/test_reference_pin.py)."""
+(tests/golden/make_golden.py, tests/test_reference_pin_gpu.py,
+tests/test_fullsize_gpu.py)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -56,3 +57,34 @@ def render(scene, params, w: int, h: int, variant: str = "strict") -> np.ndarray
     if rc != 0:
         raise RuntimeError(f"reference OpenCL run failed: {eb.value.decode()}")
     return out
+
+
+KEYS = ("vertices", "indices", "nodes", "tri_indices", "normals", "normals_indices", "materials", "tri_to_material")
+
+
+def render_subprocess(scene, params, w: int, h: int, variant: str, workdir: str, timeout: int = 300) -> np.ndarray:
+    """Run the reference kernel in a child process (the OpenCL runtime must not share a
+    process with torch's HIP runtime): the scene arrays go through an uncompressed .npz
+    in `workdir`, the frame comes back as a .npy."""
+    import subprocess
+    import sys
+    g = (lambda k: scene[k]) if isinstance(scene, dict) else (lambda k: getattr(scene, k))
+    src = os.path.join(workdir, "ref_scene.npz")
+    dst = os.path.join(workdir, "ref_out.npy")
+    np.savez(src, params=np.asarray(params, np.float32).reshape(32), w=w, h=h,
+             **{k: np.ascontiguousarray(g(k)) for k in KEYS})
+    root = os.path.dirname(HERE)
+    code = ("import sys; sys.path.insert(0, %r); from oracle import ref_ocl; ref_ocl._child(%r, %r, %r)"
+            % (root, src, dst, variant))
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+    if res.returncode != 0:
+        raise RuntimeError(f"reference kernel run failed: {res.stderr[-2000:]}")
+    out = np.load(dst)
+    os.remove(src)
+    os.remove(dst)
+    return out
+
+
+def _child(src: str, dst: str, variant: str) -> None:
+    d = dict(np.load(src))
+    np.save(dst, render(d, d["params"], int(d["w"]), int(d["h"]), variant))

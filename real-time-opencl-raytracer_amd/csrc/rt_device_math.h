@@ -241,7 +241,11 @@ __device__ __forceinline__ F3 cook_torrance_ggx(F3 n, F3 l, F3 v, F3 albedo, flo
     F3 F = F3{Fc, Fc, Fc};
     const float den = NV + 0.001f;
     const F3 sk = ((G * D) * F) * 0.25f;
-    F3 specK = F3{div_(sk.x, den), div_(sk.y, den), div_(sk.z, den)};
+    // An IEEE division in every mode, S_ref included: F is a splat of the constant f0, so
+    // the reference compiler scalarises G*D*F*0.25f/(NV+0.001f) into ONE fdiv and drops its
+    // !fpmath 2.5 on the way (the kernel's IR after AMDGPUCodeGenPrepare keeps exactly this
+    // fdiv, correctly rounded, while every other float `/` is expanded to the 2.5-ulp form).
+    F3 specK = F3{sk.x / den, sk.y / den, sk.z / den};
     F3 diffK = F3{clampf(1.0f - F.x, 0.0f, 1.0f), clampf(1.0f - F.y, 0.0f, 1.0f), clampf(1.0f - F.z, 0.0f, 1.0f)};
     const F3 md = (albedo * diffK) * NL;
     const float kPi = 3.14159274101257324219f;

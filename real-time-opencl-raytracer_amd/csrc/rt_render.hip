@@ -370,6 +370,7 @@ struct rt_ctx {
     float4* d_tris = nullptr;
     float4* d_shade = nullptr;
     int2* d_leaf = nullptr;
+    size_t n_wnodes4 = 0, n_tris4 = 0, n_shade4 = 0, n_leaf = 0, n_rank = 0;   // element counts of the scene arrays
     uint32_t root = 0;
     uint32_t n_inner = 0;
     uint32_t rank_shift = 0;   // wavefront sort keys: leaf positions >> rank_shift fit 13 bits
@@ -781,12 +782,105 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
     HIPC(c, hipMemcpy(c->d_shade, sh.data(), sh.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIPC(c, hipMemcpy(c->d_leaf, leaf_table.data(), leaf_table.size() * sizeof(int2), hipMemcpyHostToDevice));
     HIPC(c, hipMemcpy(c->d_rank, rank.data(), rank.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->n_wnodes4 = wn.size();
+    c->n_tris4 = tr.size();
+    c->n_shade4 = sh.size();
+    c->n_leaf = leaf_table.size();
+    c->n_rank = rank.size();
     c->root = ref_of[0];
     c->n_inner = (uint32_t)n_inner;
     c->rank_shift = 0;
     while (((uint64_t)std::max(nref, 1) >> c->rank_shift) > 0x1FFEu) ++c->rank_shift;
     c->fast_div = fast_ok ? 1 : 0;
     c->clean = clean ? 1 : 0;
+    c->have_scene = true;
+    ++c->scene_gen;
+    return RT_OK;
+}
+
+// ---- scene image: the uploaded device layouts as one contiguous device buffer ----
+// [header, 256 B][inner records][triangle records][shading records][escape leaves][tri ranks],
+// each section 256-B aligned.  Multi-GPU runs build the scene once and broadcast the image
+// over RCCL ("ncclBroadcast of scene buffers at load"); every rank loads it.
+namespace {
+constexpr uint32_t kImageMagic = 0x52544D49u;   // "IMTR"
+struct ImageHeader {
+    uint32_t magic, version;
+    uint64_t n_wnodes4, n_tris4, n_shade4, n_leaf, n_rank;
+    uint32_t root, n_inner, rank_shift;
+    int32_t fast_div, clean;
+};
+static_assert(sizeof(ImageHeader) <= 256, "image header fits its section");
+inline uint64_t sect(uint64_t bytes) { return (bytes + 255u) & ~uint64_t(255u); }
+uint64_t image_bytes(const ImageHeader& h) {
+    return 256 + sect(h.n_wnodes4 * 16) + sect(h.n_tris4 * 16) + sect(h.n_shade4 * 16) + sect(h.n_leaf * 8) +
+           sect(h.n_rank * 4);
+}
+}  // namespace
+
+int rt_scene_image_size(rt_ctx* c, uint64_t* bytes) {
+    if (!c || !bytes) return RT_ERR_INVALID_ARG;
+    if (!c->have_scene) return set_err(c, "rt_scene_image_size: no scene uploaded", RT_ERR_NO_SCENE);
+    ImageHeader h{kImageMagic, 1, c->n_wnodes4, c->n_tris4, c->n_shade4, c->n_leaf, c->n_rank, 0, 0, 0, 0, 0};
+    *bytes = image_bytes(h);
+    return RT_OK;
+}
+
+int rt_scene_image_pack(rt_ctx* c, void* d_image, uint64_t bytes, void* stream) {
+    if (!c || !d_image) return RT_ERR_INVALID_ARG;
+    if (!c->have_scene) return set_err(c, "rt_scene_image_pack: no scene uploaded", RT_ERR_NO_SCENE);
+    const ImageHeader h{kImageMagic, 1, c->n_wnodes4, c->n_tris4, c->n_shade4, c->n_leaf, c->n_rank,
+                        c->root, c->n_inner, c->rank_shift, c->fast_div, c->clean};
+    if (bytes < image_bytes(h)) return set_err(c, "rt_scene_image_pack: buffer too small", RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    uint8_t* p = (uint8_t*)d_image;
+    HIPC(c, hipMemcpyAsync(p, &h, sizeof h, hipMemcpyHostToDevice, s));
+    p += 256;
+    const std::pair<const void*, uint64_t> parts[] = {{c->d_wnodes, h.n_wnodes4 * 16}, {c->d_tris, h.n_tris4 * 16},
+                                                      {c->d_shade, h.n_shade4 * 16}, {c->d_leaf, h.n_leaf * 8},
+                                                      {c->d_rank, h.n_rank * 4}};
+    for (const auto& q : parts) {
+        HIPC(c, hipMemcpyAsync(p, q.first, q.second, hipMemcpyDeviceToDevice, s));
+        p += sect(q.second);
+    }
+    HIPC(c, hipStreamSynchronize(s));   // the header's host copy is a stack object
+    return RT_OK;
+}
+
+int rt_scene_image_load(rt_ctx* c, const void* d_image, uint64_t bytes, void* stream) {
+    if (!c || !d_image || bytes < 256) return set_err(c, "rt_scene_image_load: invalid argument", RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    ImageHeader h;
+    HIPC(c, hipMemcpyAsync(&h, d_image, sizeof h, hipMemcpyDeviceToHost, s));
+    HIPC(c, hipStreamSynchronize(s));
+    if (h.magic != kImageMagic || h.version != 1 || image_bytes(h) > bytes || h.n_wnodes4 == 0 || h.n_tris4 == 0 ||
+        h.n_leaf == 0 || h.n_rank == 0)
+        return set_err(c, "rt_scene_image_load: not a scene image", RT_ERR_BAD_SCENE);
+    for (auto& f : c->slots)
+        if (f.idle) HIPC(c, hipEventSynchronize(f.idle));   // frames in flight still read the old scene
+    free_scene(c);
+    HIPC(c, hipMalloc((void**)&c->d_wnodes, h.n_wnodes4 * 16));
+    HIPC(c, hipMalloc((void**)&c->d_tris, h.n_tris4 * 16));
+    HIPC(c, hipMalloc((void**)&c->d_shade, std::max<uint64_t>(h.n_shade4, 1) * 16));
+    HIPC(c, hipMalloc((void**)&c->d_leaf, h.n_leaf * 8));
+    HIPC(c, hipMalloc((void**)&c->d_rank, h.n_rank * 4));
+    const uint8_t* p = (const uint8_t*)d_image + 256;
+    const std::pair<void*, uint64_t> parts[] = {{c->d_wnodes, h.n_wnodes4 * 16}, {c->d_tris, h.n_tris4 * 16},
+                                                {c->d_shade, h.n_shade4 * 16}, {c->d_leaf, h.n_leaf * 8},
+                                                {c->d_rank, h.n_rank * 4}};
+    for (const auto& q : parts) {
+        HIPC(c, hipMemcpyAsync(q.first, p, q.second, hipMemcpyDeviceToDevice, s));
+        p += sect(q.second);
+    }
+    HIPC(c, hipStreamSynchronize(s));
+    c->n_wnodes4 = h.n_wnodes4; c->n_tris4 = h.n_tris4; c->n_shade4 = h.n_shade4; c->n_leaf = h.n_leaf; c->n_rank = h.n_rank;
+    c->root = h.root;
+    c->n_inner = h.n_inner;
+    c->rank_shift = h.rank_shift;
+    c->fast_div = h.fast_div;
+    c->clean = h.clean;
     c->have_scene = true;
     ++c->scene_gen;
     return RT_OK;

@@ -82,7 +82,8 @@ class rt_bvh_view(C.Structure):
 # every symbol include/rt_abi.h and include/rt_host.h declare
 ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_device",
                "rt_tiling_pixels", "rt_assemble_bands", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
-               "rt_comm_last_error", "rt_frame_gather", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_comm_last_error", "rt_frame_gather", "rt_scene_image_size", "rt_scene_image_pack",
+               "rt_scene_image_load", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
@@ -122,6 +123,9 @@ def lib() -> C.CDLL:
             "rt_comm_destroy": (C.c_int, [vp]),
             "rt_comm_last_error": (C.c_char_p, []),
             "rt_frame_gather": (C.c_int, [vp, vp, C.c_uint64, vp, vp, u32, u32, i32, vp]),
+            "rt_scene_image_size": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+            "rt_scene_image_pack": (C.c_int, [vp, vp, C.c_uint64, vp]),
+            "rt_scene_image_load": (C.c_int, [vp, vp, C.c_uint64, vp]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
             "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
             "rt_last_deferred": (C.c_int, [vp, C.POINTER(u32)]),
@@ -412,6 +416,21 @@ class Renderer:
             _ptr(s.nodes), s.nodes.shape[0], _ptr(s.tri_indices), s.tri_indices.size,
             _ptr(s.normals), s.normals.shape[0], _ptr(s.normals_indices), _ptr(s.materials), s.materials.shape[0],
             _ptr(s.tri_to_material)), self._h)
+
+    def scene_image_size(self) -> int:
+        """Bytes of this ctx's scene image (rt_scene_image_size)."""
+        v = C.c_uint64()
+        _check(lib().rt_scene_image_size(self._h, C.byref(v)), self._h)
+        return v.value
+
+    def pack_scene(self, d_image: int, nbytes: int, stream: Optional[int] = None) -> None:
+        """Copy the uploaded scene's device layouts into the device buffer at d_image."""
+        _check(lib().rt_scene_image_pack(self._h, C.c_void_p(d_image), nbytes, C.c_void_p(stream or None)), self._h)
+
+    def load_scene(self, d_image: int, nbytes: int, stream: Optional[int] = None) -> None:
+        """Replace this ctx's scene by a scene image (from pack_scene, e.g. broadcast by rank 0)."""
+        self._scene_keepalive = None
+        _check(lib().rt_scene_image_load(self._h, C.c_void_p(d_image), nbytes, C.c_void_p(stream or None)), self._h)
 
     def set_params(self, p):
         if isinstance(p, np.ndarray):

@@ -352,3 +352,32 @@ def test_sbvh_scene_parity(renderer, make):
     renderer.set_params(p)
     gpu = renderer.render(w, h, depth=3, flags=STRICT, aux=True)
     _compare(gpu, oracle.render(s, p, w, h, depth=3), "sbvh " + make)
+
+
+def test_scene_image_moves_the_scene_between_contexts(renderer):
+    """rt_scene_image_pack on one ctx + rt_scene_image_load on another (what bench.py does
+    across ranks, with an RCCL broadcast of the image in between): the second ctx renders
+    the same frames, in every arithmetic, without ever seeing the host arrays."""
+    import rtamd
+    import torch
+    d = load_golden("rand4k_sbvh")
+    renderer.upload(_scene(d))
+    n = renderer.scene_image_size()
+    img = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    renderer.pack_scene(img.data_ptr(), n)
+    other = rtamd.Renderer(0)
+    other.load_scene(img.data_ptr(), n)
+    del img
+    w, h = int(d["w"]), int(d["h"])
+    for r in (renderer, other):
+        r.set_params(d["params"])
+    for flags in (0, STRICT, 2, STRICT | rtamd.RT_FLAG_WAVEFRONT | rtamd.RT_FLAG_WF_SORT):
+        a = renderer.render(w, h, depth=3, flags=flags, aux=True)
+        b = other.render(w, h, depth=3, flags=flags, aux=True)
+        _compare(b, a, f"scene image flags={flags}")
+    _compare(other.render(w, h, depth=3, flags=STRICT, aux=True), _oracle(d, 3), "scene image vs oracle")
+    bad = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    with pytest.raises(rtamd.RtError):
+        other.load_scene(bad.data_ptr(), 4096)   # no magic: refused, the old scene stays
+    _compare(other.render(w, h, depth=3, flags=STRICT, aux=True), _oracle(d, 3), "after a refused image")
+    other.close()
