@@ -59,6 +59,8 @@ def parse_args(argv=None):
                     help="sbvh: the reference's SplitBVHBuilder (same bytes); binned: binned-SAH object splits")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true",
+                    help="skip the fetch trace and the gather ceiling (profiling passes: keeps other kernels out)")
     ap.add_argument("--extra-flags", type=int, default=0,
                     help="OR-ed into rt_render flags (A/B: 64 = S_strict math, 2 = S_hw math, 4 = division-form "
                          "slab test, 16 = static block order)")
@@ -482,11 +484,62 @@ def run(args, world):
     frame_rays = rays_total / args.steps
     frame_px = float(w * h) if not args.shard else float(npx)
     alg_bytes = frame_rays * bpr + 4.0 * frame_px            # reference-layout bytes per frame
-    records = frame_rays * (rec_inner + rec_tri)              # this layout's record fetches per frame
     wavefront = depth > 1 and (flags & 8)
     ns = {0: "rtk_ref", 64: "rtk_strict", 2: "rtk_hw"}[math_flags]
     kname = (f"{ns}::first_bounce_kernel<true, {'true' if depth > 1 else 'false'}>" if (depth == 1 or wavefront)
              else f"{ns}::render_kernel<true>")
+    # ---- roofline.  The path is a gather of 48-56 B records; its time is set by
+    # the vector-memory path (TA/TD), not HBM (nodes and triangles are re-read from L1/L2/Infinity
+    # Cache).  That path merges the lanes of a quad that read the same record, and a load costs
+    # per distinct record per quad (scripts/gather_peak_sweep.py), so its unit of work is a quad
+    # request.  achieved = the frame's quad requests, counted on the GPU from a trace of this
+    # frame's fetches (rt_trace_frame, a recording instantiation of the same kernel;
+    # rt_trace_stats), over ms_per_step; peak = the measured rate of quad requests when every
+    # lane reads a different record of an L2-resident table on every CU (rt_gather_peak).
+    # Both in 64-B record slots. ----
+    hbm = {"bytes_per_ray_reference_layout": round(bpr, 1),
+           "achieved_gbs": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2), "peak_gbs": HBM_PEAK_GBS,
+           "note": "SURVEY 8d algorithmic bytes of the reference layout; exceeds HBM peak because the scene is "
+                   "served from L1/L2/Infinity Cache"}
+    roof = None
+    if depth == 1 and not args.shard and not args.no_roofline:
+        r.set_params(ptab[0])
+        ft = r.fetch_trace(w, h, flags & ~16)
+        pk_ms, pk_n = r.gather_peak(16384, 256)          # 1 MiB table: L2-resident on every XCD
+        quads = ft["quad_inner"] + ft["quad_tri"]
+        peak_rps = pk_n / (pk_ms * 1e-3)   # every lane a distinct record: one quad request per lane
+        ach_rps = quads / (ms_per_step * 1e-3)
+        roof = {"bound": "l2_gather", "unit": "GB/s",
+                "achieved": round(ach_rps * 64 / 1e9, 2), "peak": round(peak_rps * 64 / 1e9, 2),
+                "frac": round(ach_rps / peak_rps, 4), "traffic": None,
+                "roof": "quad record requests of the traced frame vs random distinct records from an "
+                        "L2-resident table on every CU (rt_gather_peak)",
+                "quad_requests_per_frame": quads, "lane_fetches_per_frame": ft["inner"] + ft["tri"],
+                "lanes_per_quad_request": round((ft["inner"] + ft["tri"]) / max(1, quads), 3),
+                "wave_distinct_records_per_frame": ft["distinct_inner"] + ft["distinct_tri"],
+                "inner_fetches": ft["inner"], "tri_fetches": ft["tri"], "distinct_inner": ft["distinct_inner"],
+                "distinct_tri": ft["distinct_tri"], "wave_instructions": ft["wave_instructions"],
+                "peak_records_per_s": round(peak_rps), "peak_ns_per_record_per_cu": None,
+                "trace_max_iters": ft["max_iters"], "trace_truncated": ft["truncated"]}
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        roof["peak_ns_per_record_per_cu"] = round(cus / peak_rps * 1e9, 3)
+    if roof is None:   # wavefront bounces: no replay roof yet; the HBM model of SURVEY 8d
+        roof = {"bound": "hbm", "unit": "GB/s", "achieved": hbm["achieved_gbs"], "peak": HBM_PEAK_GBS,
+                "frac": round(hbm["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                "roof": "HBM (the fetch trace covers depth-1 frames only)"}
+    roof.update({"hbm": hbm, "stream_copy_gbs": round(stream_copy_gbs, 1), "kernel_ms": round(kernel_ms_avg, 4),
+                 "frame_kernels_ms": round(frame_ms_avg, 4), "launches_overlap": F > 1, "kernel": kname,
+                 "records_per_ray_oracle": round(rec_inner + rec_tri, 2)})
+    pmc = os.path.join(ROOT, "profiles", "r02", f"pmc_{args.config}.json")
+    if os.path.exists(pmc) and not args.orbit and not args.extra_flags:
+        try:
+            pj = json.load(open(pmc))
+            roof["traffic"] = pj.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = (f"profiles/r02/pmc_{args.config}.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                      "passes of this command (separate runs), FETCH_SIZE x2 per the guide")
+        except (OSError, ValueError):
+            pass
+
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -524,13 +577,7 @@ def run(args, world):
                    "bvh_refs": int(bvh.tri_indices.size), "bvh_build_s": round(build_s, 3),
                    "scene_source": "Collada (rt_mesh_load_dae)" if (cfg.get("dae", True) and not args.direct)
                    else "in-memory generator"},
-        "roofline": {"bound": "hbm", "achieved": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(alg_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                     "bytes_per_ray": round(bpr, 1), "records_per_ray": round(rec_inner + rec_tri, 2),
-                     "record_fetches_per_frame": round(records), "stream_copy_gbs": round(stream_copy_gbs, 1),
-                     "kernel_ms": round(kernel_ms_avg, 4), "frame_kernels_ms": round(frame_ms_avg, 4),
-                     "launches_overlap": F > 1, "kernel": kname},
+        "roofline": roof,
         "cpu_baseline": cpu,
     }
     if parity is not None:

@@ -107,6 +107,10 @@ struct Outputs {
     unsigned long long* overflow;
     uint32_t* restarts;          // traversals that outgrew the LDS stack and restarted (general code)
     uint64_t local_pixels;
+    // measurement instantiation only (rt_trace_frame): per wave [trace_cap][64] record fetches
+    uint32_t* trace;
+    uint32_t* trace_len;         // per wave: iterations recorded
+    uint32_t trace_cap;
 };
 
 __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
@@ -125,6 +129,9 @@ struct Stack {
     uint32_t* lds;      // this lane's column: lds[i * 64]
     uint32_t* glb;      // this pixel's column: glb[(i - kLdsStack) * gstride]
     uint64_t gstride;
+    uint32_t* tr_seg = nullptr;   // fetch trace (measurement instantiation): this wave's segment,
+    uint32_t* tr_it = nullptr;    //   its next free iteration (LDS word),
+    uint32_t tr_cap = 0;          //   and its capacity in iterations
     __device__ __forceinline__ uint32_t get(int i) const {
         return i < kLdsStack ? lds[i * 64] : glb[(uint64_t)(i - kLdsStack) * gstride];
     }
@@ -306,6 +313,75 @@ __global__ void __launch_bounds__(256) wf_scatter_kernel(const uint32_t* __restr
     }
 }
 
+// Fetch-trace statistics (rt_trace_stats): per wave instruction of a traced
+// frame, the lanes that fetched and the distinct records among them.  The vector-memory path
+// merges the requests of the lanes of a QUAD (lanes 4k..4k+3) that read the same record
+// (scripts/gather_peak_sweep.py: a load costs ~1.2 ns per CU per distinct record per quad, a
+// wave-uniform one ~0.16 ns per lane), so the unit of its work is a quad request.
+// Trace entries: bit 31 = triangle record, the rest a float4 index; 0xFFFFFFFF = lane idle.
+// counts: [0] inner lane-fetches, [1] triangle lane-fetches, [2] inner quad requests,
+// [3] triangle quad requests, [4] inner records distinct per wave instruction, [5] the same
+// for triangles, [6] wave instructions (iterations); summed over the frame.
+__global__ void __launch_bounds__(256) trace_stats_kernel(const uint32_t* __restrict__ trace,
+                                                          const uint32_t* __restrict__ len, uint32_t cap,
+                                                          uint32_t nwaves, unsigned long long* __restrict__ counts) {
+    const uint32_t lane = threadIdx.x & 63u, wid = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (wid >= nwaves) return;
+    const uint32_t n = min(len[wid], cap);
+    const uint32_t* seg = trace + (size_t)wid * cap * 64u + lane;
+    uint32_t c[6] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t a = seg[(size_t)i * 64u];
+        bool wave_first = true, quad_first = true;
+        for (int j = 0; j < 64; ++j) {   // a lower lane with the same record makes this one a repeat
+            const uint32_t b = (uint32_t)__shfl((int)a, j);
+            if (j < (int)lane && b == a) {
+                wave_first = false;
+                if ((uint32_t)j >> 2 == lane >> 2) quad_first = false;
+            }
+        }
+        if (a != 0xFFFFFFFFu) {
+            const uint32_t t = a >> 31;
+            c[t] += 1u;
+            c[2 + t] += quad_first ? 1u : 0u;
+            c[4 + t] += wave_first ? 1u : 0u;
+        }
+    }
+    for (int k = 0; k < 6; ++k)
+        for (int o = 32; o > 0; o >>= 1) c[k] += __shfl_xor(c[k], o);
+    if (lane == 0) {
+        for (int k = 0; k < 6; ++k) atomicAdd(counts + k, (unsigned long long)c[k]);
+        atomicAdd(counts + 6, (unsigned long long)n);
+    }
+}
+
+// Random-record gather ceiling (rt_gather_peak): every lane of every wave
+// reads a different pseudo-random record of the traversal's inner-record shape (three 16-B
+// loads + one 8-B load, 56 of 64 B) from a table of `nrec` 64-B records, `iters` times, four
+// records in flight per lane; every CU busy.  A table that fits the XCD's L2 gives the
+// ceiling of distinct-record fetches the vector-memory path can serve.
+__global__ void __launch_bounds__(256) gather_peak_kernel(const float4* __restrict__ table, uint32_t nrec,
+                                                          uint32_t iters, uint32_t* __restrict__ sink) {
+    uint32_t x = (blockIdx.x * 256u + threadIdx.x) * 2654435761u + 0x9E3779B9u;
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < iters; i += 4) {
+        float4 q[4][3];
+        float2 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+            const float4* p = table + (size_t)(x % nrec) * 4;
+            q[k][0] = p[0]; q[k][1] = p[1]; q[k][2] = p[2];
+            r[k] = *reinterpret_cast<const float2*>(p + 3);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            acc ^= __float_as_uint(q[k][0].x) ^ __float_as_uint(q[k][1].y) ^ __float_as_uint(q[k][2].z) ^
+                   __float_as_uint(r[k].y);
+    }
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;   // keeps the loads; practically never taken
+}
+
 // Band re-interleave on rank 0 (rt_assemble_bands): one block per frame row,
 // 16-B copies when rows and slots are 16-B aligned.  Pure HBM copy: 8 B/pixel.
 __global__ void __launch_bounds__(256) assemble_bands_kernel(uint32_t* __restrict__ frame,
@@ -412,6 +488,7 @@ struct rt_ctx {
     uint32_t order_tx = 0, order_ty = 0;
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
+    struct { bool on = false; uint32_t* d_trace = nullptr; uint32_t* d_len = nullptr; uint32_t cap = 0; } trace;
     bool timing_valid = false;
     std::string err;
 };
@@ -537,6 +614,7 @@ template <int M> struct Kernels;
         static void* bounce(bool fast) {                                                                   \
             return fast ? (void*)NS::wf_bounce_kernel<true> : (void*)NS::wf_bounce_kernel<false>;          \
         }                                                                                                  \
+        static void* traced() { return (void*)NS::first_bounce_kernel<true, false, true>; }               \
     };
 RTK_KERNELS(0, rtk_strict)
 RTK_KERNELS(1, rtk_hw)
@@ -548,6 +626,9 @@ static void* kernel_first(int m, bool fast, bool next) {
 }
 static void* kernel_fused(int m, bool fast) {
     return m == 0 ? Kernels<0>::fused(fast) : m == 1 ? Kernels<1>::fused(fast) : Kernels<2>::fused(fast);
+}
+static void* kernel_traced(int m) {
+    return m == 0 ? Kernels<0>::traced() : m == 1 ? Kernels<1>::traced() : Kernels<2>::traced();
 }
 static void* kernel_bounce(int m, bool fast) {
     return m == 0 ? Kernels<0>::bounce(fast) : m == 1 ? Kernels<1>::bounce(fast) : Kernels<2>::bounce(fast);
@@ -957,6 +1038,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.rgb = aux ? d_aux->rgb : nullptr;
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
+    O.trace = nullptr;
+    O.trace_len = nullptr;
+    O.trace_cap = 0;
+    const bool traced = c->trace.on;
 
     rt_ctx::FrameEv& E = c->ring[c->frames % rt_ctx::kRing];
     for (hipEvent_t& e : E.e)
@@ -1054,7 +1139,14 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.out_count = cnt + 8 * 1 + 0;
             W.bounce = 0;
             void* args[] = {&S, &F, &O, &W, &ax};
-            HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
+            if (traced) {   // rt_trace_frame: the recording instantiation of the same kernel
+                O.trace = c->trace.d_trace;
+                O.trace_len = c->trace.d_len;
+                O.trace_cap = c->trace.cap;
+                HIPC(c, hipLaunchKernel(kernel_traced(math), grid, block, args, 0, s));
+            } else {
+                HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
+            }
         }
         HIPC(c, hipEventRecord(E.e[3], s));
         E.has_k = true;
@@ -1168,6 +1260,92 @@ int rt_last_deferred(rt_ctx* c, uint32_t* count) {
     HIPC(c, hipEventSynchronize(L->idle));
     const uint64_t par = (L->nframe - 1) & 1u;   // the last frame's parity set
     HIPC(c, hipMemcpy(count, L->d_wcnt + par * kCounters + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_trace_frame(rt_ctx* c, uint32_t w, uint32_t h, uint32_t flags, uint32_t* d_trace, uint64_t trace_bytes,
+                   uint32_t cap_iters, uint32_t* d_wave_len, uint32_t* nwaves) {
+    if (!c || !d_trace || !d_wave_len || !nwaves || cap_iters == 0 || w == 0 || h == 0)
+        return set_err(c, "rt_trace_frame: invalid argument", RT_ERR_INVALID_ARG);
+    if ((flags & (RT_FLAG_WAVEFRONT | RT_FLAG_EXACT_DIV)) || !c->have_scene || !c->clean)
+        return set_err(c, "rt_trace_frame: depth-1 frames of clean scenes on the fast kernel only", RT_ERR_INVALID_ARG);
+    const uint64_t nb = (uint64_t)((w + rtk::kBlockPx - 1) / rtk::kBlockPx) * ((h + rtk::kBlockPx - 1) / rtk::kBlockPx);
+    if (trace_bytes < nb * 4 * cap_iters * 64 * 4)
+        return set_err(c, "rt_trace_frame: trace buffer smaller than waves x cap_iters x 64 x 4 B", RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->d_out, c->out_cap, (size_t)w * h);
+    if (rc) return rc;
+    HIPC(c, hipMemsetAsync(d_trace, 0xFF, nb * 4 * cap_iters * 64 * 4, c->stream));
+    c->trace.on = true;
+    c->trace.d_trace = d_trace;
+    c->trace.d_len = d_wave_len;
+    c->trace.cap = cap_iters;
+    rc = rt_render_device(c, w, h, 1, flags | RT_FLAG_STATIC_ORDER, nullptr, c->d_out, nullptr, c->stream);
+    c->trace.on = false;
+    if (rc) return rc;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    *nwaves = (uint32_t)(nb * 4);
+    return RT_OK;
+}
+
+int rt_trace_stats(rt_ctx* c, const uint32_t* d_trace, const uint32_t* d_wave_len, uint32_t nwaves, uint32_t cap_iters,
+                   uint64_t* out7) {
+    if (!c || !d_trace || !d_wave_len || nwaves == 0 || cap_iters == 0 || !out7)
+        return set_err(c, "rt_trace_stats: invalid argument", RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    unsigned long long* d_counts = nullptr;
+    HIPC(c, hipMalloc((void**)&d_counts, 7 * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d_counts, 0, 7 * sizeof(unsigned long long), c->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(rtk::trace_stats_kernel, dim3((nwaves + 3) / 4), dim3(256), 0, c->stream, d_trace, d_wave_len,
+                           cap_iters, nwaves, d_counts);
+        e = hipGetLastError();
+    }
+    unsigned long long h[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d_counts, sizeof h, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_counts);
+    if (e != hipSuccess) return set_err(c, std::string("rt_trace_stats: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    for (int k = 0; k < 7; ++k) out7[k] = h[k];
+    return RT_OK;
+}
+
+int rt_gather_peak(rt_ctx* c, uint32_t table_records, uint32_t iters, float* ms, uint64_t* records) {
+    if (!c || !ms || !records || table_records == 0 || iters == 0 || iters % 4)
+        return set_err(c, "rt_gather_peak: invalid argument", RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    int cus = 0;
+    HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    const uint32_t blocks = (uint32_t)cus * 8u;   // 8 blocks of 4 waves per CU: 8 waves per SIMD
+    float4* table = nullptr;
+    uint32_t* sink = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPC(c, hipMalloc((void**)&table, (size_t)table_records * 64));
+    hipError_t e = hipMalloc((void**)&sink, blocks * 4);
+    if (e == hipSuccess) e = hipMemsetAsync(table, 0x3C, (size_t)table_records * 64, c->stream);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(rtk::gather_peak_kernel, dim3(blocks), dim3(256), 0, c->stream, table, table_records, iters, sink);
+        e = hipEventRecord(e0, c->stream);
+    }
+    if (e == hipSuccess) {
+        for (int k = 0; k < 4; ++k)
+            hipLaunchKernelGGL(rtk::gather_peak_kernel, dim3(blocks), dim3(256), 0, c->stream, table, table_records, iters,
+                               sink);
+        e = hipEventRecord(e1, c->stream);
+    }
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float t = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(table);
+    if (sink) (void)hipFree(sink);
+    if (e != hipSuccess) return set_err(c, std::string("rt_gather_peak: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    *ms = t / 4.0f;
+    *records = (uint64_t)blocks * 256u * iters;
     return RT_OK;
 }
 

@@ -1,10 +1,10 @@
 """Copies the judged profile artefacts of scripts/profile_c3.sh into profiles/<round>/
-and writes profiles/pmc_<config>.json (HBM bytes per render-kernel launch).
+and writes profiles/<round>/pmc_<config>.json (HBM bytes per render-kernel launch).
 
 FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B/lane reads,
 MI355X_MICROARCH.md HBM section); FETCH_SIZE / WRITE_SIZE are in kB = 1024 B.
 
-    python scripts/profile_summary.py r01 [c3]
+    python scripts/profile_summary.py r02 [c3]
 """
 import csv
 import glob
@@ -15,7 +15,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "first_bounce_kernel<true, false>"   # C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray)
+KERNEL = "first_bounce_kernel<true, false, false>"   # C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray, not traced)
 
 
 def counter(d, name):
@@ -59,7 +59,7 @@ def main():
         if os.path.exists(p):
             shutil.copy(p, os.path.join(out, f"{cfg}_{log.replace('prof_', '')}"))
     res = {
-        "config": cfg, "kernel": "rtk_strict::" + KERNEL, "round": rnd,
+        "config": cfg, "kernel": "rtk_ref::" + KERNEL, "round": rnd,
         "rocprof_avg_kernel_us": None if avg_ns is None else round(avg_ns / 1e3, 2),
         "rocprof_avg_timed_window_us": timed_us,
         "hip_event_avg_timed_window_ms": hip_ms,
@@ -71,7 +71,7 @@ def main():
         "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --config " + cfg,
     }
-    json.dump(res, open(os.path.join(ROOT, "profiles", f"pmc_{cfg}.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(out, f"pmc_{cfg}.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 

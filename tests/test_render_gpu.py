@@ -381,3 +381,27 @@ def test_scene_image_moves_the_scene_between_contexts(renderer):
         other.load_scene(bad.data_ptr(), 4096)   # no magic: refused, the old scene stays
     _compare(other.render(w, h, depth=3, flags=STRICT, aux=True), _oracle(d, 3), "after a refused image")
     other.close()
+
+
+@pytest.mark.parametrize("name", ["hf40k", "cubes2_dae"])
+def test_fetch_trace_counts_the_oracles_visits(renderer, name):
+    """The recording instantiation behind the roofline (rt_trace_frame + rt_trace_stats): in S_strict
+    its inner-record fetches are exactly the oracle's inner visits (primary + shadow rays, the
+    reference's visit order) and its triangle-record fetches the oracle's triangle tests (plus
+    one per visit of an empty leaf)."""
+    from oracle import oracle
+    d = load_golden(name)
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    fr = renderer.fetch_trace(w, h, STRICT, cap_iters=512)
+    assert not fr["truncated"] and fr["wave_instructions"] > 0
+    assert 0 < fr["distinct_inner"] <= fr["quad_inner"] <= fr["inner"]
+    assert 0 < fr["distinct_tri"] <= fr["quad_tri"] <= fr["tri"]
+    st = oracle.render(d, d["params"], w, h, depth=1, aux=False)["stats"]
+    inner = st["primary"]["inner"] + st["shadow"]["inner"]
+    tris = st["primary"]["tris"] + st["shadow"]["tris"]
+    assert fr["inner"] == inner
+    assert tris <= fr["tri"] <= tris + st["primary"]["leaf"] + st["shadow"]["leaf"]
+    ms, n = renderer.gather_peak(4096, 64)
+    assert ms > 0 and n > 0
