@@ -519,6 +519,7 @@ def run(args, world):
                 "wave_distinct_records_per_frame": ft["distinct_inner"] + ft["distinct_tri"],
                 "inner_fetches": ft["inner"], "tri_fetches": ft["tri"], "distinct_inner": ft["distinct_inner"],
                 "distinct_tri": ft["distinct_tri"], "wave_instructions": ft["wave_instructions"],
+                "mixed_inner_tri_instructions": ft["mixed_instructions"],
                 "peak_records_per_s": round(peak_rps), "peak_ns_per_record_per_cu": None,
                 "trace_max_iters": ft["max_iters"], "trace_truncated": ft["truncated"]}
         cus = torch.cuda.get_device_properties(dev).multi_processor_count

@@ -216,17 +216,18 @@ int rt_timing_average(rt_ctx* ctx, int32_t n, float* total_ms, float* traverse_m
  * wave's iteration count to d_wave_len.  trace_bytes >= waves * cap_iters * 256, waves =
  * 4 * ceil(w/16) * ceil(h/16).  The pixel path itself never records (a separate kernel
  * instantiation).
- * rt_trace_stats sums over such a trace: out[0..6] = inner / triangle lane-fetches, inner /
+ * rt_trace_stats sums over such a trace: out[0..7] = inner / triangle lane-fetches, inner /
  * triangle QUAD requests (distinct records per quad of lanes per wave instruction: the
  * vector-memory path merges a quad's lanes that read one record), inner / triangle records
- * distinct per wave instruction, and wave instructions.
+ * distinct per wave instruction, wave instructions, and those whose active lanes mix inner
+ * and triangle steps.
  * rt_gather_peak measures the ceiling those distinct requests run into: every lane of 8
  * waves per SIMD on every CU reads pseudo-random inner-record-shaped records from a table of
  * table_records 64-B records, iters (multiple of 4) per lane: ms per launch and records read. */
 int rt_trace_frame(rt_ctx* ctx, uint32_t w, uint32_t h, uint32_t flags, uint32_t* d_trace, uint64_t trace_bytes,
                    uint32_t cap_iters, uint32_t* d_wave_len, uint32_t* nwaves);
 int rt_trace_stats(rt_ctx* ctx, const uint32_t* d_trace, const uint32_t* d_wave_len, uint32_t nwaves,
-                   uint32_t cap_iters, uint64_t* out7);
+                   uint32_t cap_iters, uint64_t* out8);
 int rt_gather_peak(rt_ctx* ctx, uint32_t table_records, uint32_t iters, float* ms, uint64_t* records);
 
 /* Traversals of the last frame that outgrew the fast kernel's LDS stack and

@@ -321,7 +321,8 @@ __global__ void __launch_bounds__(256) wf_scatter_kernel(const uint32_t* __restr
 // Trace entries: bit 31 = triangle record, the rest a float4 index; 0xFFFFFFFF = lane idle.
 // counts: [0] inner lane-fetches, [1] triangle lane-fetches, [2] inner quad requests,
 // [3] triangle quad requests, [4] inner records distinct per wave instruction, [5] the same
-// for triangles, [6] wave instructions (iterations); summed over the frame.
+// for triangles, [6] wave instructions (iterations), [7] iterations whose active lanes mix
+// inner and triangle steps (both code paths issue); summed over the frame.
 __global__ void __launch_bounds__(256) trace_stats_kernel(const uint32_t* __restrict__ trace,
                                                           const uint32_t* __restrict__ len, uint32_t cap,
                                                           uint32_t nwaves, unsigned long long* __restrict__ counts) {
@@ -329,9 +330,12 @@ __global__ void __launch_bounds__(256) trace_stats_kernel(const uint32_t* __rest
     if (wid >= nwaves) return;
     const uint32_t n = min(len[wid], cap);
     const uint32_t* seg = trace + (size_t)wid * cap * 64u + lane;
-    uint32_t c[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t c[6] = {0, 0, 0, 0, 0, 0}, mixed = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t a = seg[(size_t)i * 64u];
+        const uint64_t tri_lanes = __builtin_amdgcn_ballot_w64(a != 0xFFFFFFFFu && (a >> 31) != 0);
+        const uint64_t inner_lanes = __builtin_amdgcn_ballot_w64(a != 0xFFFFFFFFu && (a >> 31) == 0);
+        mixed += (tri_lanes != 0 && inner_lanes != 0) ? 1u : 0u;
         bool wave_first = true, quad_first = true;
         for (int j = 0; j < 64; ++j) {   // a lower lane with the same record makes this one a repeat
             const uint32_t b = (uint32_t)__shfl((int)a, j);
@@ -352,6 +356,7 @@ __global__ void __launch_bounds__(256) trace_stats_kernel(const uint32_t* __rest
     if (lane == 0) {
         for (int k = 0; k < 6; ++k) atomicAdd(counts + k, (unsigned long long)c[k]);
         atomicAdd(counts + 6, (unsigned long long)n);
+        atomicAdd(counts + 7, (unsigned long long)mixed);
     }
 }
 
@@ -1289,24 +1294,24 @@ int rt_trace_frame(rt_ctx* c, uint32_t w, uint32_t h, uint32_t flags, uint32_t* 
 }
 
 int rt_trace_stats(rt_ctx* c, const uint32_t* d_trace, const uint32_t* d_wave_len, uint32_t nwaves, uint32_t cap_iters,
-                   uint64_t* out7) {
-    if (!c || !d_trace || !d_wave_len || nwaves == 0 || cap_iters == 0 || !out7)
+                   uint64_t* out8) {
+    if (!c || !d_trace || !d_wave_len || nwaves == 0 || cap_iters == 0 || !out8)
         return set_err(c, "rt_trace_stats: invalid argument", RT_ERR_INVALID_ARG);
     HIPC(c, hipSetDevice(c->device));
     unsigned long long* d_counts = nullptr;
-    HIPC(c, hipMalloc((void**)&d_counts, 7 * sizeof(unsigned long long)));
-    hipError_t e = hipMemsetAsync(d_counts, 0, 7 * sizeof(unsigned long long), c->stream);
+    HIPC(c, hipMalloc((void**)&d_counts, 8 * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d_counts, 0, 8 * sizeof(unsigned long long), c->stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(rtk::trace_stats_kernel, dim3((nwaves + 3) / 4), dim3(256), 0, c->stream, d_trace, d_wave_len,
                            cap_iters, nwaves, d_counts);
         e = hipGetLastError();
     }
-    unsigned long long h[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (e == hipSuccess) e = hipMemcpyAsync(h, d_counts, sizeof h, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d_counts);
     if (e != hipSuccess) return set_err(c, std::string("rt_trace_stats: ") + hipGetErrorString(e), RT_ERR_DEVICE);
-    for (int k = 0; k < 7; ++k) out7[k] = h[k];
+    for (int k = 0; k < 8; ++k) out8[k] = h[k];
     return RT_OK;
 }
 

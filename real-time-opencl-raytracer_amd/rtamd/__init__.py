@@ -445,13 +445,14 @@ class Renderer:
         nw = C.c_uint32()
         _check(lib().rt_trace_frame(self._h, w, h, flags, C.c_void_p(trace.data_ptr()), trace.numel() * 4, cap_iters,
                                     C.c_void_p(wlen.data_ptr()), C.byref(nw)), self._h)
-        out = (C.c_uint64 * 7)()
+        out = (C.c_uint64 * 8)()
         _check(lib().rt_trace_stats(self._h, C.c_void_p(trace.data_ptr()), C.c_void_p(wlen.data_ptr()), nw.value,
                                     cap_iters, out), self._h)
         max_it = int(wlen.max().item())
         del trace, wlen
         return {"inner": int(out[0]), "tri": int(out[1]), "quad_inner": int(out[2]), "quad_tri": int(out[3]),
                 "distinct_inner": int(out[4]), "distinct_tri": int(out[5]), "wave_instructions": int(out[6]),
+                "mixed_instructions": int(out[7]),
                 "max_iters": max_it, "cap_iters": cap_iters, "waves": nw.value, "truncated": max_it > cap_iters}
 
     def gather_peak(self, table_records: int = 16384, iters: int = 256):
