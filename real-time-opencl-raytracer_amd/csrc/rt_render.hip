@@ -251,9 +251,10 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
 // ---- math-independent kernels ----
 
 // Per-bounce ray sort of the wavefront path (RT_FLAG_WF_SORT): counting sort of the
-// queue's live entries by an 8-bit key, the direction octant (3 bits) above the top 5
-// bits of the leaf position of the triangle the ray leaves from (coarsened to 13 bits by
-// the host's shift), so that a wave's rays start close together and travel the same way.
+// queue's live entries by an 8-bit key, the top 5 bits of the leaf position of the
+// triangle the ray leaves from (its hit node; coarsened to 13 bits by the host's shift)
+// above the direction octant (3 bits), so that a wave's rays start close together and
+// travel the same way.
 // wf_hist_kernel: per-block LDS histogram -> global hist[256]; stores each entry's key.
 // wf_scatter_kernel: every block takes a contiguous range of each bucket for its own
 // entries (one atomic on the bucket's cursor past the exclusive prefix of hist) and
@@ -264,7 +265,7 @@ __device__ __forceinline__ uint32_t wf_key8(const QRay& r, const uint32_t* __res
     const int hit = __float_as_int(r.c.w);
     const uint32_t oct = (r.b.x < 0.0f ? 4u : 0u) | (r.b.y < 0.0f ? 2u : 0u) | (r.b.z < 0.0f ? 1u : 0u);
     const uint32_t pos13 = hit >= 0 ? min(rank[hit / 3] >> shift, 0x1FFEu) : 0x1FFEu;
-    return (oct << 5) | (pos13 >> 8);
+    return ((pos13 >> 8) << 3) | oct;   // position first: C5 1.13 ms vs 1.18 octant-first, 1.15 position only
 }
 
 __global__ void __launch_bounds__(256) wf_hist_kernel(const QRay* __restrict__ q, const uint32_t* __restrict__ count,

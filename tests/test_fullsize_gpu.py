@@ -12,7 +12,7 @@ Two pins per config:
     frames of C3/C4 are then tied to it through their first bounce (hit ids and t of a
     depth-1 frame == bounce 0 of the pinned depth-3 frame).
 C4 is rendered as 2-, 4- and 8-way band shards re-interleaved by rt_assemble_bands (the
-multi-GPU frame path); C5 in the wavefront mode with per-bounce ray sorting.
+multi-GPU frame path); C5 in the wavefront mode, with and without the per-bounce ray sort.
 """
 import os
 
@@ -92,9 +92,9 @@ def test_strict_matches_oracle_whole_frame(renderer, name):
     ref = oracle.render(scene, params, w, h, depth=depth, flags=cfg["flags"])
     _compare(gpu, ref, name)
     assert int((gpu["hits"][:, 0, 0] >= 0).sum()) > 0.5 * w * h or name == "c2"   # the frame is mostly scene
-    if name == "c5":   # the adaptive block order's second frame, and the unsorted wavefront
+    if name == "c5":   # the adaptive block order's second frame, and the per-bounce sorted wavefront
         _compare(renderer.render(w, h, depth=depth, flags=cfg["flags"] | STRICT, aux=True), ref, "c5 (2nd frame)")
-        _compare(renderer.render(w, h, depth=depth, flags=WAVEFRONT | STRICT, aux=True), ref, "c5 unsorted")
+        _compare(renderer.render(w, h, depth=depth, flags=WAVEFRONT | WF_SORT | STRICT, aux=True), ref, "c5 sorted")
 
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5"])
@@ -107,12 +107,14 @@ def test_default_math_matches_reference_kernel(renderer, name, tmp_path):
     ref = _reference(scene, params, w, h, tmp_path)
     renderer.upload(scene)
     renderer.set_params(params)
-    flags = (WAVEFRONT | WF_SORT) if name == "c5" else 0
+    flags = cfg["flags"] & (WAVEFRONT | WF_SORT)
     out = renderer.render(w, h, depth=3, flags=flags)
     nd = int(np.sum(out != ref))
     print(f"{name}: S_ref depth 3 vs reference kernel: {nd} of {out.size} pixels differ")
     assert nd == 0
     assert int(np.sum(renderer.render(w, h, depth=3, flags=flags ^ WAVEFRONT if flags else WAVEFRONT) != ref)) == 0
+    if name == "c5":   # and the per-bounce sorted wavefront
+        assert int(np.sum(renderer.render(w, h, depth=3, flags=WAVEFRONT | WF_SORT) != ref)) == 0
     if cfg["depth"] == 1:
         # the depth-1 frame's rays are bounce 0 of the pinned depth-3 frame
         d3 = renderer.render(w, h, depth=3, aux=True)
