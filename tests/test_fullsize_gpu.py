@@ -101,7 +101,7 @@ def test_strict_matches_oracle_whole_frame(renderer, name):
 def test_default_math_matches_reference_kernel(renderer, name, tmp_path):
     """S_ref (rt_render's default arithmetic) against the reference kernel as its host
     builds it, the whole frame at depth 3 with shadows (the reference's compiled-in
-    setting), on the config's scene and camera; C5 through its wavefront + sort path."""
+    setting), on the config's scene and camera; C5 through its wavefront path, unsorted and sorted."""
     scene, params, cfg = _config(name)
     w, h = cfg["w"], cfg["h"]
     ref = _reference(scene, params, w, h, tmp_path)
