@@ -15,11 +15,13 @@ line through; under torchrun, WORLD_SIZE must equal --gpus.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -48,9 +50,23 @@ def parse_args(argv=None):
     ap.add_argument("--band-rows", type=int, default=8,
                     help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
     ap.add_argument("--dist", action="store_true", help="use the process-group gather path even at N = 1")
-    ap.add_argument("--gather", default="torch", choices=["torch", "native"],
-                    help="band exchange at N > 1: torch.distributed gather (async, RCCL) + rt_assemble_bands, or "
-                         "the library's own RCCL communicators on the frame's stream (rt_frame_gather)")
+    ap.add_argument("--gather", default="torch", choices=["torch", "native", "ipc"],
+                    help="band exchange at N > 1: torch.distributed gather (async, RCCL) + rt_assemble_bands; "
+                         "native: the library's own RCCL communicator (rt_frame_exchange: gathers in frame order "
+                         "on its stream, rank 0's assembly on another, joined to the render streams by events); "
+                         "ipc: no collective, every rank copies its bands straight into rank 0's frame, mapped "
+                         "through a HIP IPC handle (rt_bands_put)")
+    ap.add_argument("--pg", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for setup and timing; gloo lets a rehearsal run N ranks on one "
+                         "GPU (RCCL refuses two ranks on one device)")
+    ap.add_argument("--gather-batch", type=int, default=4,
+                    help="frames per exchange at N > 1: one gather carries B consecutive frames of a stream, so "
+                         "the exchange's host cost is paid once per B frames")
+    ap.add_argument("--local-batch", action="store_true",
+                    help="diagnostic: batches of --gather-batch frames per stream at N = 1 too (no exchange)")
+    ap.add_argument("--hang-timeout", type=float, default=600.0,
+                    help="N > 1: a rank that has not finished this many seconds after joining the process group "
+                         "exits with status 3 (a stuck collective ends the run instead of hanging it)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="frames in flight (one stream each): frame i+1 renders while frame i drains / gathers")
     ap.add_argument("--shard", default="", help="R/N: render only rank R's bands of an N-way split (diagnostic)")
@@ -97,6 +113,12 @@ def _probe(args):
     dist.destroy_process_group()
 
 
+def _hang_exit(rank, seconds):
+    print(f"bench.py: rank {rank} still running {seconds:.0f} s after joining the process group; exiting",
+          file=sys.stderr, flush=True)
+    os._exit(3)
+
+
 def main():
     args = parse_args()
     world_env = os.environ.get("WORLD_SIZE")
@@ -112,10 +134,15 @@ def main():
     if args.probe_launch:
         _probe(args)
         return
-    run(args, world)
+    # the result is the ONE line on stdout: everything else the process writes to fd 1 (RCCL's
+    # version banner on the first communicator, library messages) goes to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    run(args, world, result_out)
 
 
-def run(args, world):
+def run(args, world, result_out=None):
     # Frames in flight run on separate streams; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
     # queues (4 by default, and exported as 4 on the GPU boxes; shared with torch's and the
     # library's own streams), so with four frames in flight two would share a queue and
@@ -149,7 +176,29 @@ def run(args, world):
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(args.pg, device_id=dev if args.pg == "nccl" else None,
+                                timeout=datetime.timedelta(seconds=args.hang_timeout))
+        watchdog = threading.Timer(args.hang_timeout, _hang_exit, (rank, args.hang_timeout))
+        watchdog.daemon = True
+        watchdog.start()
+    pg_cpu = args.pg == "gloo"
+
+    def bcast(t):   # device tensors through the process group (gloo: staged through host memory)
+        if pg_cpu:
+            c = t.cpu()
+            dist.broadcast(c, src=0)
+            t.copy_(c)
+        else:
+            dist.broadcast(t, src=0)
+
+    def allreduce(t, op):
+        if pg_cpu:
+            c = t.cpu()
+            dist.all_reduce(c, op=op)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, op=op)
+
     cfg = configs.CONFIGS[args.config]
     w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"] | args.extra_flags
     math_flags = flags & (64 | 2)
@@ -181,15 +230,15 @@ def run(args, world):
         if rank == 0:
             nb[0] = r.scene_image_size()
             nb[1] = ptab.shape[0]
-        dist.broadcast(nb, src=0)
+        bcast(nb)
         scene_bytes = int(nb[0].item())
         img = torch.empty(scene_bytes, dtype=torch.uint8, device=dev)
         pt = torch.empty((int(nb[1].item()), 32), dtype=torch.float32, device=dev)
         if rank == 0:
             r.pack_scene(img.data_ptr(), scene_bytes, torch.cuda.current_stream().cuda_stream)
             pt.copy_(torch.from_numpy(ptab))
-        dist.broadcast(img, src=0)
-        dist.broadcast(pt, src=0)
+        bcast(img)
+        bcast(pt)
         if rank != 0:
             torch.cuda.synchronize(dev)
             r.load_scene(img.data_ptr(), scene_bytes)
@@ -199,7 +248,9 @@ def run(args, world):
     r.set_params(ptab[0])
 
     # --shard R/N (diagnostic, world 1 only): render just shard R of an N-way band split,
-    # i.e. one rank's kernel work at N GPUs without the gather
+    # i.e. one rank's kernel work at N GPUs without the gather; with --dist
+    # (R = 0) also rank 0's exchange work at N GPUs: its own slot gathered, the whole frame
+    # assembled from N slots (the other N-1 slots hold no peer data: no frame check)
     shard_r, shard_n = rank, world
     if args.shard:
         if world != 1:
@@ -209,22 +260,103 @@ def run(args, world):
     npx = rtamd.tiling_pixels(w, h, shard_r, shard_n, args.band_rows)
     cap = rtamd.tiling_pixels(w, h, 0, shard_n, args.band_rows)  # rank 0 owns the most bands
     cap = (cap + 3) // 4 * 4                                     # 16-B aligned gather slots
-    # Frames in flight: frame i runs on stream i % F (each stream has its own frame scratch in
-    # the library, rt_render_device), so frame i+1's render overlaps frame i's tail and, at N > 1,
-    # frame i's RCCL gather.  Every launch of a frame -- render, the gather's ordering (RCCL waits
-    # on torch's current stream) and rank 0's assembly -- is on that frame's stream.  (torch's
-    # default stream is handle 0, which the C ABI would read as "the ctx's own stream".)
+    # Frames in flight: batch i of B frames runs on stream i % F (each stream has its own frame
+    # scratch in the library, rt_render_device), so its renders overlap the other streams' frames
+    # and, at N > 1, the RCCL gathers of earlier batches.  (torch's default stream is handle 0,
+    # which the C ABI would read as "the ctx's own stream".)
     F = max(1, args.inflight)
+    native = use_dist and args.gather == "native"
+    comms = []
+    if native:
+        # ONE communicator per rank (rt_frame_exchange: gathers in frame order on its own
+        # stream); rank 0's id travels through the process group's store.  If any rank cannot
+        # create it, every rank falls back to the torch.distributed gather (agreed through an
+        # all-reduce, so no rank is left waiting).
+        store = dist.distributed_c10d._get_default_store()
+        ok = 1.0
+        try:
+            if rank == 0:   # an empty id tells every rank not to enter the collective init
+                try:
+                    uid0 = rtamd.Comm.unique_id()
+                except rtamd.RtError:
+                    uid0 = b""
+                store.set("rtamd_comm", uid0)
+            uid = bytes(store.get("rtamd_comm"))
+            if len(uid) != rtamd.Comm.ID_BYTES:
+                raise rtamd.RtError(-2, "rank 0 has no RCCL id")
+            comms.append(rtamd.Comm(local, world, rank, uid))
+        except rtamd.RtError as e:
+            print(f"rank {rank}: native band exchange unavailable ({e}); using torch.distributed", file=sys.stderr)
+            ok = 0.0
+        flag = torch.tensor([ok], device=dev)
+        allreduce(flag, dist.ReduceOp.MIN)
+        if flag.item() < 1.0:
+            native = False
+            for c in comms:
+                c.close()
+            comms = []
+    ipc = use_dist and args.gather == "ipc"
+    tgather = use_dist and not native and not ipc
+    # frames per exchange: a batch of B consecutive frames renders on one stream into one
+    # (B, cap) buffer and one gather carries the whole batch, so the exchange's host cost
+    # (~0.05 ms per gather with its event waits; a 1/8 shard's frame is ~0.05 ms) is paid
+    # once per B frames
+    # (ipc: a frame's put is one copy issued right after its render, no batching)
+    B = max(1, args.gather_batch) if ((use_dist and not ipc) or args.local_batch) else 1
+    # buffer sets: batch i uses set i % NB.  At N > 1 the sets cycle 2F ways, so a batch never
+    # renders into a set whose gather was issued less than F batches earlier: the gathers run
+    # in issue order on one RCCL stream (the process group's, or the rt_comm's), and a render
+    # waiting on the latest one would tie the streams into lock-step.  Rank 0 assembles on a
+    # stream of its own.
+    NB = 2 * F if use_dist else F
     streams = [torch.cuda.Stream(dev) for _ in range(F)]
     torch.cuda.set_stream(streams[0])
-    outs = [torch.zeros(cap, dtype=torch.int32, device=dev) for _ in range(F)]
-    # rank 0: per in-flight frame one contiguous (world, cap) gather target, re-interleaved into
-    # that frame's framebuffer by one rt_assemble_bands launch
-    gbufs = [torch.zeros(world, cap, dtype=torch.int32, device=dev) for _ in range(F)] \
-        if (use_dist and rank == 0) else None
-    glists = [list(g.unbind(0)) for g in gbufs] if gbufs is not None else [None] * F
-    frames = [torch.zeros(h * w, dtype=torch.int32, device=dev) for _ in range(F)] \
-        if (rank == 0 and use_dist) else None
+    outs = [torch.zeros(B, cap, dtype=torch.int32, device=dev) for _ in range(NB)]
+    # rank 0: per buffer set one contiguous (world, B * cap) gather target, re-interleaved
+    # into the set's B framebuffers by one rt_assemble_bands_batch launch
+    gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)] \
+        if (use_dist and rank == 0 and not ipc) else None
+    glists = [list(g.unbind(0))[:world] for g in gbufs] if gbufs is not None else [None] * NB
+    frames_all = torch.zeros(NB, B, h * w, dtype=torch.int32, device=dev) if (rank == 0 and use_dist) else None
+    frames = list(frames_all) if frames_all is not None else None
+    shared = None
+    if ipc:
+        # rank 0's framebuffers mapped into every rank (rt_ipc_export / rt_ipc_open): each
+        # rank's bands go straight to their rows of rank 0's frame.  If any rank cannot map
+        # them, every rank falls back to the torch.distributed gather.
+        store = dist.distributed_c10d._get_default_store()
+        ok = 1.0
+        try:
+            if rank == 0:
+                try:
+                    hnd, off = rtamd.SharedFrames.export(local, frames_all.data_ptr())
+                    store.set("rtamd_ipc", hnd + off.to_bytes(8, "little"))
+                except rtamd.RtError:
+                    store.set("rtamd_ipc", b"")
+                    raise
+                fr_base = frames_all.data_ptr()
+            else:
+                blob = bytes(store.get("rtamd_ipc"))
+                if len(blob) != rtamd.SharedFrames.HANDLE_BYTES + 8:
+                    raise rtamd.RtError(-2, "rank 0 could not export its frames")
+                shared = rtamd.SharedFrames.open(local, blob[:-8], int.from_bytes(blob[-8:], "little"))
+                fr_base = shared.ptr
+        except rtamd.RtError as e:
+            print(f"rank {rank}: frame mapping unavailable ({e}); using torch.distributed", file=sys.stderr)
+            ok = 0.0
+        flag = torch.tensor([ok], device=dev)
+        allreduce(flag, dist.ReduceOp.MIN)
+        if flag.item() < 1.0:   # (B stays 1)
+            ipc, tgather = False, True
+            if shared is not None:
+                shared.close()
+                shared = None
+            if rank == 0:
+                gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)]
+                glists = [list(g.unbind(0))[:world] for g in gbufs]
+        else:
+            put = rtamd.bands_putter(w, h, tiling)
+            put_dst = [[fr_base + 4 * (j * B + s) * h * w for s in range(B)] for j in range(NB)]
 
     # rays traced by this rank in a frame with params p (counted with the aux planes, untimed)
     d = max(depth, 1)
@@ -242,92 +374,97 @@ def run(args, world):
 
     rays_f0, prim_f0 = count_rays(ptab[0])
 
-    # One step = one frame: render this rank's bands -> (N > 1) async RCCL gather of the bands
-    # to rank 0 -> rank 0 re-interleaves them into the frame.  A slot's previous frame is
-    # finished (gather waited on, assembled) before the slot's buffers are reused.
-    pending = [None] * F
+    # One step = one frame: render this rank's bands -> (N > 1) RCCL gather of the bands to
+    # rank 0 -> rank 0 re-interleaves them into the frame.
+    pending = [None] * NB     # torch path: the gather work of set j's last batch
+    filled = [0] * NB         # frames in set j's last batch
+    asm_used = [False] * NB
+    cur = [0, 0]              # (batch number, frames rendered in it)
     nstep = [0]
     # the per-frame host path, with everything constant bound once: at N = 8 a frame is
     # ~0.05 ms of GPU time, so the host's enqueue per frame has to stay well under that
     launch = r.frame_launcher(w, h, depth, flags, tiling)
     sh = [st.cuda_stream for st in streams]
-    out_ptr = [o.data_ptr() for o in outs]
+    out_ptr = [[o[s].data_ptr() for s in range(B)] for o in outs]
+    outs_ptr = [o.data_ptr() for o in outs]
     orbit_params = [rtamd.array_to_params(p) for p in ptab] if args.orbit else None
     set_params = rtamd.lib().rt_set_params
     hdl = r._h
-    if use_dist:
+    if native:
+        slots_ptr = [g.data_ptr() for g in gbufs] if rank == 0 else [0] * NB
+        fr_ptr = [f.data_ptr() for f in frames] if rank == 0 else [0] * NB
+        # (--shard: the one-rank communicator assembles this rank's own bands only)
+        slot_wait, xchg = comms[0].frame_exchanger(cap, w, cap // w if args.shard else h, args.band_rows)
+    if tgather:
         pg = dist.distributed_c10d._get_default_group()
         gopts = dist.GatherOptions()
         gopts.rootRank = 0
         gopts.asyncOp = True
-        g_out = [[glists[k]] if rank == 0 else [] for k in range(F)]
-        g_in = [[o] for o in outs]
+        g_out = [[glists[j]] if rank == 0 else [] for j in range(NB)]
+        g_in = [[o.view(-1)] for o in outs]
         if rank == 0:
-            assemble = rtamd.bands_assembler(w, h, world, args.band_rows, cap)
+            assemble = rtamd.bands_assembler(w, h, shard_n, args.band_rows, B * cap, cap)
             frame_ptr = [f.data_ptr() for f in frames]
             gbuf_ptr = [g.data_ptr() for g in gbufs]
+            asm_stream = torch.cuda.Stream(dev)
+            asm_sh = asm_stream.cuda_stream
+            asm_done = [torch.cuda.Event() for _ in range(NB)]
 
-    native = use_dist and args.gather == "native"
-    comms = []
-    if native:
-        # one communicator per in-flight stream; rank 0's ids travel through the process
-        # group's store.  If any rank cannot create them, every rank falls back to the
-        # torch.distributed gather (agreed through an all-reduce, so no rank is left waiting).
-        store = dist.distributed_c10d._get_default_store()
-        ok = 1.0
-        try:
-            for k in range(F):
-                key = f"rtamd_comm_{k}"
-                if rank == 0:   # an empty id tells every rank not to enter the collective init
-                    try:
-                        uid0 = rtamd.Comm.unique_id()
-                    except rtamd.RtError:
-                        uid0 = b""
-                    store.set(key, uid0)
-                uid = bytes(store.get(key))
-                if len(uid) != rtamd.Comm.ID_BYTES:
-                    raise rtamd.RtError(-2, "rank 0 has no RCCL id")
-                comms.append(rtamd.Comm(local, world, rank, uid))
-        except rtamd.RtError as e:
-            print(f"rank {rank}: native band exchange unavailable ({e}); using torch.distributed", file=sys.stderr)
-            ok = 0.0
-        flag = torch.tensor([ok], device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if flag.item() < 1.0:
-            native = False
-            for c in comms:
-                c.close()
-            comms = []
-        slots_ptr = [g.data_ptr() for g in gbufs] if rank == 0 else [0] * F
-        fr_ptr = [f.data_ptr() for f in frames] if rank == 0 else [0] * F
-
-    def finish(k):
-        work, pending[k] = pending[k], None
-        work.wait()   # orders streams[k] (the current stream) after the gather
+    def exchange(j, k, nfr):
+        """Set j's batch (nfr frames, rendered on stream k = the current stream) to rank 0."""
+        filled[j] = nfr
+        if ipc:      # this rank's bands into their rows of rank 0's frame, after the render
+            for s in range(nfr):
+                put(out_ptr[j][s], put_dst[j][s], sh[k])
+            return
+        if native:   # gather on the rt_comm's stream after the renders, rank 0's assembly after it
+            xchg(j, nfr, outs_ptr[j], slots_ptr[j], fr_ptr[j], sh[k])
+            return
+        # dist.gather(outs[j], glists[j], dst=0, async_op=True) without its argument checks,
+        # then rank 0 assembles the frames on its assembly stream
+        if rank == 0 and asm_used[j]:   # the set's previous assembly has read gbufs[j]
+            streams[k].wait_event(asm_done[j])
+        work = pg.gather(g_out[j], g_in[j], gopts)
+        pending[j] = work
         if rank == 0:
-            assemble(frame_ptr[k], gbuf_ptr[k], sh[k])
+            torch.cuda.set_stream(asm_stream)
+            work.wait()   # the assembly stream after the gather
+            assemble(frame_ptr[j], gbuf_ptr[j], asm_sh, nfr)
+            asm_done[j].record(asm_stream)
+            asm_used[j] = True
+            torch.cuda.set_stream(streams[k])
 
     def step():
         n = nstep[0]
-        k = n % F
         nstep[0] += 1
-        torch.cuda.set_stream(streams[k])
-        if pending[k] is not None:
-            finish(k)
+        b, s = cur
+        k, j = b % F, b % NB
+        if s == 0:
+            torch.cuda.set_stream(streams[k])
+            if pending[j] is not None:   # set j's last gather (NB batches ago) has read outs[j]
+                pending[j].wait()
+                pending[j] = None
+            elif native:                 # likewise, through the rt_comm's events
+                slot_wait(j, sh[k])
         if orbit_params is not None:   # updateCamera (RayTracer.cpp:609-672) for this frame
             set_params(hdl, orbit_params[n])
-        launch(out_ptr[k], sh[k])
-        if native:     # gather + assembly on the frame's own stream: no cross-stream waits
-            comms[k].frame_gather(out_ptr[k], cap, slots_ptr[k], fr_ptr[k], w, h, args.band_rows, sh[k])
-        elif use_dist:   # dist.gather(outs[k], glists[k], dst=0, async_op=True) without its argument checks
-            pending[k] = pg.gather(g_out[k], g_in[k], gopts)
+        launch(out_ptr[j][s], sh[k])
+        s += 1
+        if s < B:
+            cur[1] = s
+            return
+        if use_dist:
+            exchange(j, k, B)
+        else:
+            filled[j] = B
+        cur[0], cur[1] = b + 1, 0
 
     def drain():
-        for j in range(F):
-            k = (nstep[0] + j) % F   # oldest first
-            if pending[k] is not None:
-                torch.cuda.set_stream(streams[k])
-                finish(k)
+        """Send a part-filled batch as it is; the caller then synchronises the device."""
+        b, s = cur
+        if s and use_dist:
+            exchange(b % NB, b % F, s)
+        cur[0], cur[1] = b + (1 if s else 0), 0
 
     for _ in range(args.warmup):
         step()
@@ -366,11 +503,12 @@ def run(args, world):
 
     # check (untimed): rank 0's assembled frames equal its own one-rank render of the frame
     frame_ok = None
-    if use_dist and rank == 0 and not args.orbit:
+    if use_dist and rank == 0 and not args.orbit and not args.shard:
         full = torch.zeros(h * w, dtype=torch.int32, device=dev)
         r.render_device(w, h, depth, flags, full.data_ptr(), stream=streams[0].cuda_stream)
         torch.cuda.synchronize(dev)
-        frame_ok = all(bool(torch.equal(full, f)) for f in frames)
+        frame_ok = sum(filled) > 0 and all(bool(torch.equal(full, frames[j][s]))
+                                           for j in range(NB) for s in range(filled[j]))
 
     # (untimed for `value`) the reference's own boundary: rt_render, synchronous, the frame
     # read back into host memory (raytrace_gpgpu: launch + clFinish + clEnqueueReadBuffer,
@@ -394,13 +532,13 @@ def run(args, world):
     if use_dist:
         t = torch.tensor([elapsed, float(rays_local), float(prim_local)], dtype=torch.float64, device=dev)
         tmax = t[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        allreduce(tmax, dist.ReduceOp.MAX)
         tsum = t[1:].clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        allreduce(tsum, dist.ReduceOp.SUM)
         elapsed = float(tmax.item())
         rays_total, prim_total = float(tsum[0].item()), float(tsum[1].item())
         km = torch.tensor([kernel_ms_avg], dtype=torch.float64, device=dev)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        allreduce(km, dist.ReduceOp.MAX)
         kernel_ms_avg = float(km.item())
     else:
         rays_total, prim_total = float(rays_local), float(prim_local)
@@ -409,6 +547,8 @@ def run(args, world):
     value = rays_total / elapsed / 1e6
 
     if rank != 0:
+        if shared is not None:   # unmapped before rank 0 may free its frames
+            shared.close()
         if world > 1:
             dist.barrier()
             for c in comms:
@@ -486,7 +626,7 @@ def run(args, world):
     alg_bytes = frame_rays * bpr + 4.0 * frame_px            # reference-layout bytes per frame
     wavefront = depth > 1 and (flags & 8)
     ns = {0: "rtk_ref", 64: "rtk_strict", 2: "rtk_hw"}[math_flags]
-    kname = (f"{ns}::first_bounce_kernel<true, {'true' if depth > 1 else 'false'}>" if (depth == 1 or wavefront)
+    kname = (f"{ns}::first_bounce_kernel<true, {'true' if depth > 1 else 'false'}, false>" if (depth == 1 or wavefront)
              else f"{ns}::render_kernel<true>")
     # ---- roofline.  The path is a gather of 48-56 B records; its time is set by
     # the vector-memory path (TA/TD), not HBM (nodes and triangles are re-read from L1/L2/Infinity
@@ -566,9 +706,12 @@ def run(args, world):
                    "mpixels_per_s": round(w * h * args.steps / elapsed / 1e6, 1),
                    "parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
                                    else f"shard {args.shard} of the band split (diagnostic, no gather)"),
-                   "band_rows": args.band_rows, "frames_in_flight": F,
-                   "band_exchange": (None if not use_dist else "rt_frame_gather (library RCCL communicators)" if native
-                                     else "torch.distributed gather (RCCL) + rt_assemble_bands"),
+                   "band_rows": args.band_rows, "frames_in_flight": F, "frames_per_gather": B, "buffer_sets": NB,
+                   "band_exchange": (None if not use_dist else "rt_frame_exchange (one library RCCL communicator, gather + assembly streams)" if native
+                                     else "rt_bands_put: each rank's bands copied straight into rank 0's frame "
+                                          "(HIP IPC mapping, no collective)" if ipc
+                                     else "torch.distributed gather (RCCL), B frames per gather, + rt_assemble_bands on rank 0's "
+                                     "assembly stream"),
                    "scene_distribution": (f"rank 0 builds; {scene_bytes} B scene image broadcast over RCCL "
                                           "(rt_scene_image_pack / _load)" if world > 1 else "single rank"),
                    "scene_setup_s": round(scene_s, 3),
@@ -587,7 +730,7 @@ def run(args, world):
         res["config"]["gathered_frame_equals_single_rank_render"] = frame_ok
     if host_boundary is not None:
         res["config"]["host_boundary"] = host_boundary
-    print(json.dumps(res))
+    print(json.dumps(res), file=result_out or sys.stdout, flush=True)
     if use_dist:
         dist.barrier()
         for c in comms:

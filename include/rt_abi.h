@@ -179,22 +179,60 @@ int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* tiling);
  * hands to glDrawPixels).  Asynchronous: returns after enqueue. */
 int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint32_t w, uint32_t h,
                       int32_t nranks, int32_t band_rows, void* stream);
+/* The same for nframes frames in one launch: rank r's slot (at d_slots + r*slot_pixels)
+ * holds the frames' band buffers frame_pixels apart; d_frame receives nframes frames of
+ * w*h pixels, one after the other. */
+int rt_assemble_bands_batch(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint64_t frame_pixels,
+                            int32_t nframes, uint32_t w, uint32_t h, int32_t nranks, int32_t band_rows, void* stream);
 
 /* Native band exchange for multi-GPU frames over RCCL: the reference
  * reads the frame back to the host (RayTracer.cpp:343); here every rank's bands go to
- * rank 0 on the frame's own stream.  One rt_comm per in-flight stream (a communicator's
- * operations are serialised); the 128-byte id travels from rank 0 to the others over any
- * channel (bench.py: the torch.distributed store). */
+ * rank 0, which re-interleaves them into the frame.  The 128-byte id travels from rank 0
+ * to the others over any channel (bench.py: the torch.distributed store). */
 typedef struct rt_comm rt_comm;
 int rt_comm_unique_id(uint8_t* id, int32_t id_bytes);
+/* One communicator per rank, with its own gather stream and (rank 0) assembly stream,
+ * both at the device's highest stream priority. */
 int rt_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* id, int32_t id_bytes, rt_comm** out);
 int rt_comm_destroy(rt_comm* comm);
 const char* rt_comm_last_error(void);
-/* ncclGather of slot_pixels pixels from every rank's d_bands into rank 0's d_slots
- * (nranks * slot_pixels), then on rank 0 rt_assemble_bands into d_frame; all on `stream`.
- * Every rank calls it once per frame, in the same order. */
+/* The frame path (bench.py --gather native).  The caller cycles buffer sets, "slots"
+ * 0..63, each carrying a batch of nframes consecutive frames: slot j = one band buffer
+ * d_bands of nframes * frame_pixels (every rank; frame f's bands at f * frame_pixels) and,
+ * on rank 0, one (nranks * nframes * frame_pixels) d_slots + nframes * w*h d_frames.
+ * On the batch's render stream:
+ *   rt_frame_slot_wait(comm, j, stream)   -- the stream waits for slot j's last gather
+ *                                            (it read d_bands), not for later ones;
+ *   rt_render_device(..., d_bands + f * frame_pixels, ..., stream) for each frame f;
+ *   rt_frame_exchange(comm, j, nframes, ...) -- after the renders: ncclGather to rank 0 on
+ *                                            the communicator's stream (issue order = batch
+ *                                            order, the same on every rank), then rank 0's
+ *                                            rt_assemble_bands_batch on its assembly stream.
+ * rt_frame_ready_wait(comm, j, stream): a consumer stream waits for slot j's frames
+ * (rank 0: assembled; other ranks: sent).  All calls return after enqueue. */
+int rt_frame_exchange(rt_comm* comm, int32_t slot, int32_t nframes, const uint32_t* d_bands, uint64_t frame_pixels,
+                      uint32_t* d_slots, uint32_t* d_frames, uint32_t w, uint32_t h, int32_t band_rows, void* stream);
+int rt_frame_slot_wait(rt_comm* comm, int32_t slot, void* stream);
+int rt_frame_ready_wait(rt_comm* comm, int32_t slot, void* stream);
+/* The same exchange entirely on `stream` (gather, then rank 0's assembly), for a caller with
+ * one stream per communicator.  Every rank calls it once per frame, in the same order. */
 int rt_frame_gather(rt_comm* comm, const uint32_t* d_bands, uint64_t slot_pixels, uint32_t* d_slots,
                     uint32_t* d_frame, uint32_t w, uint32_t h, int32_t band_rows, void* stream);
+
+/* Collective-free frame exchange (bench.py --gather ipc).  Rank 0 exports its framebuffers
+ * with rt_ipc_export (the 64-byte handle of the allocation they lie in + their offset in it)
+ * and passes both to the other ranks (any channel), which map the allocation with rt_ipc_open
+ * (d_base; the frames are at d_base + offset); then every rank, after rendering a frame's
+ * bands, places them into rank 0's frame with rt_bands_put on its own stream: one strided
+ * device copy (the rank's bands are evenly spaced in the frame) plus one for a short last
+ * band.  Rank 0 puts its own bands the same way into its local frame.  A frame is complete
+ * when every rank's put has completed (bench.py: device synchronise + barrier).  Replaces
+ * the host readback of RayTracer.cpp:343 for a frame rendered on N GPUs. */
+int rt_ipc_export(int32_t device, void* d_ptr, uint8_t* handle, int32_t handle_bytes, uint64_t* offset);
+int rt_ipc_open(int32_t device, const uint8_t* handle, int32_t handle_bytes, void** d_base);
+int rt_ipc_close(int32_t device, void* d_base);
+int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
+                 void* stream);
 
 /* Kernel-side timing of the last render, from HIP events on the launch stream
  * (ms): total_ms = every kernel of the frame (counter reset / block-order

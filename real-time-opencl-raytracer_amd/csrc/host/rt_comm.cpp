@@ -1,13 +1,25 @@
 // rt_comm.cpp -- native band exchange for multi-GPU frames over RCCL (xGMI).
 //
 // The frame's one real exchange (the reference reads the frame back to the
-// host, RayTracer.cpp:343) issued from C++ on the frame's own stream: ncclGather of every
-// rank's band buffer into rank 0's slots, then (rank 0) rt_assemble_bands into the frame.
-// Render, gather and assembly of one frame are then ordered by one stream with no
-// cross-stream waits, and a frame costs the host three C calls.  A communicator serves one
-// stream at a time (RCCL serialises a communicator's operations), so a caller with frames
-// in flight creates one rt_comm per in-flight stream.  torch.distributed (or any other
-// channel) only carries the 128-byte id from rank 0 to the others.
+// host, RayTracer.cpp:343), issued from C++: ncclGather of every rank's band buffer into
+// rank 0's slots, then (rank 0) rt_assemble_bands into the frame.
+//
+// rt_frame_exchange (the bench path): ONE communicator per rank, its gathers in issue order
+// on the communicator's own stream, rank 0's assemblies on a second stream; the frame's
+// render stream is joined to them by events only.  The caller cycles buffer sets ("slots"):
+// a frame's render into slot j waits (rt_frame_slot_wait) only for the gather that last read
+// slot j, issued several frames earlier, so render streams never wait on the latest gather.
+// A frame costs the host three C calls (render, slot wait, exchange).
+//
+// rt_frame_gather: the same exchange on the caller's stream (one stream per communicator).
+// torch.distributed (or any other channel) only carries the 128-byte id from rank 0.
+//
+// rt_bands_put (bench.py --gather ipc): no collective at all.  Rank 0's framebuffers are
+// exported once as a HIP IPC handle (rt_ipc_alloc / rt_ipc_open); every rank then copies its
+// bands straight to their rows of rank 0's frame with ONE strided copy per frame on its own
+// stream (a rank's bands are evenly spaced: dst pitch = nranks * band).  Over xGMI the copy
+// runs on the sending GPU; rank 0 runs no receive kernel and no re-interleave, and no kernel
+// anywhere spins waiting for a peer.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
@@ -17,9 +29,26 @@
 #include "rt_abi.h"
 
 struct rt_comm {
+    static constexpr int kSlots = 64;
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    hipStream_t xs = nullptr;   // gathers, in issue order
+    hipStream_t xa = nullptr;   // rank 0: assemblies
+    hipEvent_t ready[kSlots] = {}, gathered[kSlots] = {}, assembled[kSlots] = {};
+    bool sent[kSlots] = {}, built[kSlots] = {};
 };
+
+static void comm_release(rt_comm* c) {
+    for (int i = 0; i < rt_comm::kSlots; ++i) {
+        if (c->ready[i]) (void)hipEventDestroy(c->ready[i]);
+        if (c->gathered[i]) (void)hipEventDestroy(c->gathered[i]);
+        if (c->assembled[i]) (void)hipEventDestroy(c->assembled[i]);
+    }
+    if (c->xs) (void)hipStreamDestroy(c->xs);
+    if (c->xa) (void)hipStreamDestroy(c->xa);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+}
 
 static std::string g_comm_err;
 
@@ -57,14 +86,30 @@ int rt_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* 
     c->nranks = nranks;
     c->rank = rank;
     c->device = device;
+    // the exchange streams at the device's highest priority: a gather or assembly is a few
+    // workgroups that should not queue behind the next frame's render waves
+    int lo = 0, hi = 0;
+    bool ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+              hipStreamCreateWithPriority(&c->xs, hipStreamNonBlocking, hi) == hipSuccess &&
+              hipStreamCreateWithPriority(&c->xa, hipStreamNonBlocking, hi) == hipSuccess;
+    for (int i = 0; ok && i < rt_comm::kSlots; ++i)
+        ok = hipEventCreateWithFlags(&c->ready[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->gathered[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->assembled[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        comm_release(c);
+        return comm_err("rt_comm_create: exchange streams / events", RT_ERR_DEVICE);
+    }
     *out = c;
     return RT_OK;
 }
 
 int rt_comm_destroy(rt_comm* c) {
     if (!c) return RT_ERR_INVALID_ARG;
-    if (c->comm) (void)ncclCommDestroy(c->comm);
-    delete c;
+    (void)hipSetDevice(c->device);
+    if (c->xs) (void)hipStreamSynchronize(c->xs);
+    if (c->xa) (void)hipStreamSynchronize(c->xa);
+    comm_release(c);
     return RT_OK;
 }
 
@@ -80,6 +125,115 @@ int rt_frame_gather(rt_comm* c, const uint32_t* d_bands, uint64_t slot_pixels, u
         const int rc = rt_assemble_bands(d_frame, d_slots, slot_pixels, w, h, c->nranks, band_rows, stream);
         if (rc) return comm_err(std::string("rt_assemble_bands: ") + rt_last_error(nullptr), rc);
     }
+    return RT_OK;
+}
+
+int rt_frame_exchange(rt_comm* c, int32_t slot, int32_t nframes, const uint32_t* d_bands, uint64_t frame_pixels,
+                      uint32_t* d_slots, uint32_t* d_frames, uint32_t w, uint32_t h, int32_t band_rows, void* stream) {
+    if (!c || slot < 0 || slot >= rt_comm::kSlots || nframes < 1 || !d_bands || frame_pixels == 0 || w == 0 || h == 0 ||
+        band_rows < 1)
+        return comm_err("rt_frame_exchange: invalid argument", RT_ERR_INVALID_ARG);
+    const bool root = c->rank == 0;
+    if (root && (!d_slots || !d_frames)) return comm_err("rt_frame_exchange: rank 0 needs slots and frames", RT_ERR_INVALID_ARG);
+    const uint64_t slot_pixels = (uint64_t)nframes * frame_pixels;   // one rank's share of the gather
+    // the gather after the frames' renders; on rank 0 also after the slot's previous assembly
+    // (it read d_slots)
+    if (hipEventRecord(c->ready[slot], (hipStream_t)stream) != hipSuccess ||
+        hipStreamWaitEvent(c->xs, c->ready[slot], 0) != hipSuccess ||
+        (root && c->built[slot] && hipStreamWaitEvent(c->xs, c->assembled[slot], 0) != hipSuccess))
+        return comm_err("rt_frame_exchange: stream ordering", RT_ERR_DEVICE);
+    const ncclResult_t r = ncclGather(d_bands, root ? d_slots : nullptr, slot_pixels, ncclUint32, 0, c->comm, c->xs);
+    if (r != ncclSuccess) return comm_err(std::string("ncclGather: ") + ncclGetErrorString(r), RT_ERR_DEVICE);
+    if (hipEventRecord(c->gathered[slot], c->xs) != hipSuccess)
+        return comm_err("rt_frame_exchange: event record", RT_ERR_DEVICE);
+    c->sent[slot] = true;
+    if (root) {
+        if (hipStreamWaitEvent(c->xa, c->gathered[slot], 0) != hipSuccess)
+            return comm_err("rt_frame_exchange: stream ordering", RT_ERR_DEVICE);
+        const int rc = rt_assemble_bands_batch(d_frames, d_slots, slot_pixels, frame_pixels, nframes, w, h, c->nranks,
+                                               band_rows, c->xa);
+        if (rc) return comm_err(std::string("rt_assemble_bands: ") + rt_last_error(nullptr), rc);
+        if (hipEventRecord(c->assembled[slot], c->xa) != hipSuccess)
+            return comm_err("rt_frame_exchange: event record", RT_ERR_DEVICE);
+        c->built[slot] = true;
+    }
+    return RT_OK;
+}
+
+int rt_frame_slot_wait(rt_comm* c, int32_t slot, void* stream) {
+    if (!c || slot < 0 || slot >= rt_comm::kSlots) return comm_err("rt_frame_slot_wait: invalid argument", RT_ERR_INVALID_ARG);
+    if (c->sent[slot] && hipStreamWaitEvent((hipStream_t)stream, c->gathered[slot], 0) != hipSuccess)
+        return comm_err("rt_frame_slot_wait: stream ordering", RT_ERR_DEVICE);
+    return RT_OK;
+}
+
+int rt_frame_ready_wait(rt_comm* c, int32_t slot, void* stream) {
+    if (!c || slot < 0 || slot >= rt_comm::kSlots) return comm_err("rt_frame_ready_wait: invalid argument", RT_ERR_INVALID_ARG);
+    hipEvent_t ev = c->rank == 0 ? c->assembled[slot] : c->gathered[slot];
+    const bool done = c->rank == 0 ? c->built[slot] : c->sent[slot];
+    if (done && hipStreamWaitEvent((hipStream_t)stream, ev, 0) != hipSuccess)
+        return comm_err("rt_frame_ready_wait: stream ordering", RT_ERR_DEVICE);
+    return RT_OK;
+}
+
+int rt_ipc_export(int32_t device, void* d_ptr, uint8_t* handle, int32_t handle_bytes, uint64_t* offset) {
+    if (!d_ptr || !handle || !offset || handle_bytes < (int32_t)sizeof(hipIpcMemHandle_t))
+        return comm_err("rt_ipc_export: invalid argument", RT_ERR_INVALID_ARG);
+    if (hipSetDevice(device) != hipSuccess) return comm_err("rt_ipc_export: hipSetDevice", RT_ERR_DEVICE);
+    // the handle names the whole allocation d_ptr lies in (a caching allocator's segment)
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d_ptr);
+    if (e != hipSuccess) return comm_err(std::string("rt_ipc_export: hipMemGetAddressRange: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    hipIpcMemHandle_t h;
+    if ((e = hipIpcGetMemHandle(&h, (void*)base)) != hipSuccess)
+        return comm_err(std::string("rt_ipc_export: hipIpcGetMemHandle: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    std::memcpy(handle, &h, sizeof h);
+    *offset = (uint64_t)((uintptr_t)d_ptr - (uintptr_t)base);
+    return RT_OK;
+}
+
+int rt_ipc_open(int32_t device, const uint8_t* handle, int32_t handle_bytes, void** d_ptr) {
+    if (!d_ptr || !handle || handle_bytes < (int32_t)sizeof(hipIpcMemHandle_t))
+        return comm_err("rt_ipc_open: invalid argument", RT_ERR_INVALID_ARG);
+    *d_ptr = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return comm_err("rt_ipc_open: hipSetDevice", RT_ERR_DEVICE);
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof h);
+    const hipError_t e = hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return comm_err(std::string("rt_ipc_open: hipIpcOpenMemHandle: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    return RT_OK;
+}
+
+int rt_ipc_close(int32_t device, void* d_ptr) {
+    if (!d_ptr) return RT_ERR_INVALID_ARG;
+    (void)hipSetDevice(device);
+    return hipIpcCloseMemHandle(d_ptr) == hipSuccess ? RT_OK : comm_err("rt_ipc_close: hipIpcCloseMemHandle", RT_ERR_DEVICE);
+}
+
+int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
+                 void* stream) {
+    if (!d_bands || !d_frame || w == 0 || h == 0) return comm_err("rt_bands_put: invalid argument", RT_ERR_INVALID_ARG);
+    const int32_t N = tiling && tiling->nranks > 1 ? tiling->nranks : 1;
+    const int32_t r = N > 1 ? tiling->rank : 0;
+    const uint32_t R = N > 1 ? (uint32_t)tiling->band_rows : h;
+    if (r < 0 || r >= N || R == 0) return comm_err("rt_bands_put: bad tiling", RT_ERR_INVALID_ARG);
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t nb = (h + R - 1) / R;                   // bands in the frame; band b = rank b % N
+    const uint32_t mine = nb > (uint32_t)r ? (nb - 1 - r) / N + 1 : 0;
+    if (mine == 0) return RT_OK;
+    const uint32_t last = r + (mine - 1) * N;              // this rank's last band
+    const bool short_last = (uint64_t)(last + 1) * R > h;  // the frame's last band may be short
+    const uint32_t full = mine - (short_last ? 1 : 0);
+    const size_t band_bytes = (size_t)R * w * 4;
+    hipError_t e = hipSuccess;
+    if (full)
+        e = hipMemcpy2DAsync(d_frame + (size_t)r * R * w, band_bytes * N, d_bands, band_bytes, band_bytes, full,
+                             hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && short_last)
+        e = hipMemcpyAsync(d_frame + (size_t)last * R * w, d_bands + (size_t)full * R * w,
+                           (size_t)(h - last * R) * w * 4, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return comm_err(std::string("rt_bands_put: ") + hipGetErrorString(e), RT_ERR_DEVICE);
     return RT_OK;
 }
 

@@ -388,20 +388,22 @@ __global__ void __launch_bounds__(256) gather_peak_kernel(const float4* __restri
     if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;   // keeps the loads; practically never taken
 }
 
-// Band re-interleave on rank 0 (rt_assemble_bands): one block per frame row,
-// 16-B copies when rows and slots are 16-B aligned.  Pure HBM copy: 8 B/pixel.
+// Band re-interleave on rank 0 (rt_assemble_bands[_batch]): one block per frame row and
+// frame (grid h x nframes), 16-B copies when rows and slots are 16-B aligned.  Pure HBM
+// copy: 8 B/pixel.  Rank r's slot starts at r * slot_pixels and holds the frames' band
+// buffers frame_pixels apart.
 __global__ void __launch_bounds__(256) assemble_bands_kernel(uint32_t* __restrict__ frame,
                                                              const uint32_t* __restrict__ slots, uint64_t slot_pixels,
-                                                             uint32_t w, uint32_t h, uint32_t nranks,
-                                                             uint32_t band_rows) {
+                                                             uint64_t frame_pixels, uint32_t w, uint32_t h,
+                                                             uint32_t nranks, uint32_t band_rows) {
     const uint32_t y = blockIdx.x;
     if (y >= h) return;
     const uint32_t band = y / band_rows;
     const uint32_t rank = band % nranks;
     const uint64_t local_row = (uint64_t)(band / nranks) * band_rows + (y % band_rows);
-    const uint32_t* src = slots + (uint64_t)rank * slot_pixels + local_row * w;
-    uint32_t* dst = frame + (uint64_t)y * w;
-    if ((w & 3u) == 0 && (slot_pixels & 3u) == 0) {
+    const uint32_t* src = slots + (uint64_t)rank * slot_pixels + blockIdx.y * frame_pixels + local_row * w;
+    uint32_t* dst = frame + (uint64_t)blockIdx.y * w * h + (uint64_t)y * w;
+    if ((w & 3u) == 0 && (slot_pixels & 3u) == 0 && (frame_pixels & 3u) == 0) {
         const uint4* s4 = reinterpret_cast<const uint4*>(src);
         uint4* d4 = reinterpret_cast<uint4*>(dst);
         for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
@@ -442,9 +444,11 @@ __global__ void __launch_bounds__(256) assemble_bands_kernel(uint32_t* __restric
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // per-frame timing events, a ring over the last kRing frames:
-    // e[0]/e[1] around all kernels of the frame, e[2]/e[3] around the main render kernel
-    struct FrameEv { hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr}; bool has_k = false; };
+    // per-frame timing events, a ring over the last kRing frames: e[0]/e[1] around all
+    // kernels of the frame; e[2] after the main render kernel when more kernels follow it
+    // (has_k; the main kernel is the frame's first, so it spans e[0]..e[2]).  Two records per
+    // depth-1 frame: each costs host time on the per-frame path.
+    struct FrameEv { hipEvent_t e[3] = {nullptr, nullptr, nullptr}; bool has_k = false; };
     static constexpr int kRing = 64;
     FrameEv ring[kRing];
     uint64_t frames = 0;
@@ -644,21 +648,28 @@ extern "C" {
 
 int rt_abi_version(void) { return 2; }
 
-int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint32_t w, uint32_t h,
-                      int32_t nranks, int32_t band_rows, void* stream) {
-    if (!d_frame || !d_slots || w == 0 || h == 0 || nranks < 1 || band_rows < 1)
+int rt_assemble_bands_batch(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint64_t frame_pixels,
+                            int32_t nframes, uint32_t w, uint32_t h, int32_t nranks, int32_t band_rows, void* stream) {
+    if (!d_frame || !d_slots || w == 0 || h == 0 || nranks < 1 || band_rows < 1 || nframes < 1 || nframes > 65535)
         return set_err(nullptr, "rt_assemble_bands: invalid argument", RT_ERR_INVALID_ARG);
-    // every rank's bands must fit its slot (rt_tiling_pixels of the fullest rank)
+    // every rank's bands must fit a frame's buffer (rt_tiling_pixels of the fullest rank),
+    // and a rank's frames its slot
     rt_tiling t0{0, nranks, band_rows, 0};
-    if ((uint64_t)rt_tiling_pixels(w, h, &t0) > slot_pixels)
+    const uint64_t need = (uint64_t)rt_tiling_pixels(w, h, &t0);
+    if (need > frame_pixels || (uint64_t)nframes * frame_pixels > slot_pixels)
         return set_err(nullptr, "rt_assemble_bands: slot_pixels smaller than rank 0's bands", RT_ERR_INVALID_ARG);
     if (((uintptr_t)d_frame | (uintptr_t)d_slots) & 15u)
         return set_err(nullptr, "rt_assemble_bands: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
-    hipLaunchKernelGGL(rtk::assemble_bands_kernel, dim3(h), dim3(256), 0, (hipStream_t)stream, d_frame, d_slots,
-                       slot_pixels, w, h, (uint32_t)nranks, (uint32_t)band_rows);
+    hipLaunchKernelGGL(rtk::assemble_bands_kernel, dim3(h, nframes), dim3(256), 0, (hipStream_t)stream, d_frame, d_slots,
+                       slot_pixels, frame_pixels, w, h, (uint32_t)nranks, (uint32_t)band_rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(nullptr, std::string("rt_assemble_bands: ") + hipGetErrorString(e), RT_ERR_DEVICE);
     return RT_OK;
+}
+
+int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint32_t w, uint32_t h,
+                      int32_t nranks, int32_t band_rows, void* stream) {
+    return rt_assemble_bands_batch(d_frame, d_slots, slot_pixels, slot_pixels, 1, w, h, nranks, band_rows, stream);
 }
 
 const char* rt_last_error(rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
@@ -1115,11 +1126,8 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     HIPC(c, hipEventRecord(E.e[0], s));
 
     if (!wavefront) {
-        HIPC(c, hipEventRecord(E.e[2], s));
         void* args[] = {&S, &F, &O, &ax};
         HIPC(c, hipLaunchKernel(kernel_fused(math, fast), grid, block, args, 0, s));
-        HIPC(c, hipEventRecord(E.e[3], s));
-        E.has_k = true;
     } else {
         // Wavefront: bounce 0 over tiles, then one persistent launch per further bounce
         // over the queue of rays still in flight.
@@ -1138,7 +1146,6 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             if ((rc = ensure(c, L.d_perm, L.perm_cap, (size_t)npix))) return rc;
         }
         auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)L.d_wq[k & 1] : (rtk::QRay*)nullptr; };
-        HIPC(c, hipEventRecord(E.e[2], s));
         {
             rtk::WQ W{};
             W.out = depth > 1 ? qbuf(1) : nullptr;
@@ -1154,8 +1161,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
                 HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
             }
         }
-        HIPC(c, hipEventRecord(E.e[3], s));
-        E.has_k = true;
+        if (depth > 1) {
+            HIPC(c, hipEventRecord(E.e[2], s));
+            E.has_k = true;
+        }
         // the bounce launches take no part in the adaptive order or the counter clearing
         rtk::Frame Fb = F;
         Fb.tile_cost = nullptr;
@@ -1226,7 +1235,7 @@ static int frame_times(rt_ctx* c, uint64_t f, float& total, float& kernel) {
     HIPC(c, hipEventSynchronize(E.e[1]));
     HIPC(c, hipEventElapsedTime(&total, E.e[0], E.e[1]));
     kernel = total;
-    if (E.has_k) HIPC(c, hipEventElapsedTime(&kernel, E.e[2], E.e[3]));
+    if (E.has_k) HIPC(c, hipEventElapsedTime(&kernel, E.e[0], E.e[2]));
     return RT_OK;
 }
 

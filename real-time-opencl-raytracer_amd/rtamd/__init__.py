@@ -81,8 +81,10 @@ class rt_bvh_view(C.Structure):
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
 ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_device",
-               "rt_tiling_pixels", "rt_assemble_bands", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
-               "rt_comm_last_error", "rt_frame_gather", "rt_scene_image_size", "rt_scene_image_pack",
+               "rt_tiling_pixels", "rt_assemble_bands", "rt_assemble_bands_batch", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
+               "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
+               "rt_frame_ready_wait", "rt_ipc_export", "rt_ipc_open", "rt_ipc_close", "rt_bands_put",
+               "rt_scene_image_size", "rt_scene_image_pack",
                "rt_scene_image_load", "rt_trace_frame", "rt_trace_stats", "rt_gather_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
@@ -118,11 +120,19 @@ def lib() -> C.CDLL:
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
             "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
             "rt_assemble_bands": (C.c_int, [vp, vp, C.c_uint64, u32, u32, i32, i32, vp]),
+            "rt_assemble_bands_batch": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, i32, u32, u32, i32, i32, vp]),
             "rt_comm_unique_id": (C.c_int, [vp, i32]),
             "rt_comm_create": (C.c_int, [i32, i32, i32, vp, i32, C.POINTER(vp)]),
             "rt_comm_destroy": (C.c_int, [vp]),
             "rt_comm_last_error": (C.c_char_p, []),
             "rt_frame_gather": (C.c_int, [vp, vp, C.c_uint64, vp, vp, u32, u32, i32, vp]),
+            "rt_frame_exchange": (C.c_int, [vp, i32, i32, vp, C.c_uint64, vp, vp, u32, u32, i32, vp]),
+            "rt_frame_slot_wait": (C.c_int, [vp, i32, vp]),
+            "rt_ipc_export": (C.c_int, [i32, vp, vp, i32, C.POINTER(C.c_uint64)]),
+            "rt_ipc_open": (C.c_int, [i32, vp, i32, C.POINTER(vp)]),
+            "rt_ipc_close": (C.c_int, [i32, vp]),
+            "rt_bands_put": (C.c_int, [vp, vp, u32, u32, vp, vp]),
+            "rt_frame_ready_wait": (C.c_int, [vp, i32, vp]),
             "rt_scene_image_size": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
             "rt_scene_image_pack": (C.c_int, [vp, vp, C.c_uint64, vp]),
             "rt_scene_image_load": (C.c_int, [vp, vp, C.c_uint64, vp]),
@@ -582,12 +592,93 @@ class Comm:
         if rc:
             raise RtError(rc, lib().rt_comm_last_error().decode())
 
+    def frame_exchanger(self, frame_pixels: int, w: int, h: int, band_rows: int):
+        """Callables (slot_wait(slot, stream), exchange(slot, nframes, d_bands, d_slots, d_frames,
+        stream)) for rt_frame_slot_wait / rt_frame_exchange with their constant arguments bound
+        once."""
+        L, hdl = lib(), self._h
+        fx, fw = L.rt_frame_exchange, L.rt_frame_slot_wait
+        a = (C.c_uint64(frame_pixels),)
+        b = (C.c_uint32(w), C.c_uint32(h), C.c_int32(band_rows))
+
+        def slot_wait(slot: int, stream: int) -> None:
+            _stream_arg(stream)
+            rc = fw(hdl, slot, stream)
+            if rc:
+                raise RtError(rc, L.rt_comm_last_error().decode())
+
+        def exchange(slot: int, nframes: int, d_bands: int, d_slots: int, d_frames: int, stream: int) -> None:
+            _stream_arg(stream)
+            rc = fx(hdl, slot, nframes, d_bands, *a, d_slots or None, d_frames or None, *b, stream)
+            if rc:
+                raise RtError(rc, L.rt_comm_last_error().decode())
+        return slot_wait, exchange
+
+    def ready_wait(self, slot: int, stream: int) -> None:
+        """rt_frame_ready_wait: `stream` waits for slot's frame (rank 0: assembled)."""
+        _stream_arg(stream)
+        rc = lib().rt_frame_ready_wait(self._h, slot, stream)
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+
     def close(self):
         if getattr(self, "_h", None) and _lib is not None:
             _lib.rt_comm_destroy(self._h)
             self._h = None
 
     __del__ = close
+
+
+class SharedFrames:
+    """Device memory of rank 0 mapped into the other ranks' processes (rt_ipc_*,
+    include/rt_abi.h): rank 0 exports a buffer it owns (a torch tensor's data_ptr) with
+    SharedFrames.export(...) -> (handle, offset); another process maps it with
+    SharedFrames.open(device, handle, offset) and writes through .ptr."""
+
+    HANDLE_BYTES = 64
+
+    @staticmethod
+    def export(device: int, d_ptr: int):
+        buf = (C.c_uint8 * SharedFrames.HANDLE_BYTES)()
+        off = C.c_uint64()
+        rc = lib().rt_ipc_export(device, d_ptr, buf, SharedFrames.HANDLE_BYTES, C.byref(off))
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+        return bytes(buf), off.value
+
+    def __init__(self, device: int, base: int, offset: int):
+        self.device, self.base, self.ptr = device, base, base + offset
+
+    @classmethod
+    def open(cls, device: int, handle: bytes, offset: int) -> "SharedFrames":
+        buf = (C.c_uint8 * cls.HANDLE_BYTES).from_buffer_copy(handle)
+        p = C.c_void_p()
+        rc = lib().rt_ipc_open(device, buf, cls.HANDLE_BYTES, C.byref(p))
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+        return cls(device, p.value, offset)
+
+    def close(self):
+        if getattr(self, "base", None) and _lib is not None:
+            _lib.rt_ipc_close(self.device, self.base)
+            self.base = self.ptr = None
+
+    __del__ = close
+
+
+def bands_putter(w: int, h: int, tiling: Optional[rt_tiling] = None):
+    """A callable (d_bands, d_frame, stream) -> None for rt_bands_put with its constant
+    arguments built once: this rank's bands into their rows of a (local or mapped) frame."""
+    fn = lib().rt_bands_put
+    tl = None if tiling is None else C.byref(tiling)
+    a = (C.c_uint32(w), C.c_uint32(h), tl)
+
+    def put(d_bands: int, d_frame: int, stream: int) -> None:
+        _stream_arg(stream)
+        rc = fn(d_bands, d_frame, *a, stream)
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+    return put
 
 
 def _stream_arg(stream):
@@ -605,15 +696,16 @@ def assemble_bands_device(d_frame: int, d_slots: int, slot_pixels: int, w: int, 
                                    C.c_void_p(stream or None)))
 
 
-def bands_assembler(w: int, h: int, nranks: int, band_rows: int, slot_pixels: int):
-    """A callable (d_frame, d_slots, stream) -> None for rt_assemble_bands with its constant
-    arguments built once."""
-    fn = lib().rt_assemble_bands
-    a = (C.c_uint64(slot_pixels), C.c_uint32(w), C.c_uint32(h), C.c_int32(nranks), C.c_int32(band_rows))
+def bands_assembler(w: int, h: int, nranks: int, band_rows: int, slot_pixels: int, frame_pixels: int = 0):
+    """A callable (d_frames, d_slots, stream[, nframes]) -> None for rt_assemble_bands_batch
+    with its constant arguments built once (frame_pixels 0 = slot_pixels: one frame per slot)."""
+    fn = lib().rt_assemble_bands_batch
+    a = (C.c_uint64(slot_pixels), C.c_uint64(frame_pixels or slot_pixels))
+    b = (C.c_uint32(w), C.c_uint32(h), C.c_int32(nranks), C.c_int32(band_rows))
 
-    def assemble(d_frame: int, d_slots: int, stream: int) -> None:
+    def assemble(d_frames: int, d_slots: int, stream: int, nframes: int = 1) -> None:
         _stream_arg(stream)
-        rc = fn(d_frame, d_slots, *a, stream)
+        rc = fn(d_frames, d_slots, *a, nframes, *b, stream)
         if rc:
             _check(rc)
     return assemble

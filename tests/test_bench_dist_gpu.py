@@ -1,8 +1,12 @@
-"""bench.py's multi-GPU frame path on one GPU: a one-rank RCCL process group, the async
-band gather into rank 0's slots, rt_assemble_bands, four frames in flight -- the code the
-driver's N = 2..8 runs execute -- with the assembled frames checked against a one-rank
-render (bench.py's `gathered_frame_equals_single_rank_render`).  Runs bench.py as a child
-process on a small config (C2 scene, 1080p, a few frames)."""
+"""bench.py's multi-GPU frame path on one GPU, with the assembled frames checked against a
+one-rank render (bench.py's `gathered_frame_equals_single_rank_render`).  Runs bench.py as
+a child process on a small config (C2 scene, 1080p, a few frames):
+  * one rank through every exchange -- the torch.distributed gather (batches of B frames,
+    a part-filled last batch), the library's RCCL communicator (rt_frame_exchange), the
+    IPC band puts (rt_bands_put) -- on a one-rank RCCL process group;
+  * 2 and 3 ranks sharing the GPU (a gloo process group: RCCL refuses two ranks on one
+    device) through the IPC band puts: rank 0's frames mapped into the other processes,
+    every rank's bands copied into them -- the driver's N > 1 code path, end to end."""
 import json
 import os
 import subprocess
@@ -16,7 +20,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("i,extra", [(0, []), (1, ["--inflight", "1"]), (2, ["--band-rows", "16"]),
-                                     (3, ["--gather", "native"]), (4, ["--gather", "native", "--inflight", "1"])])
+                                     (3, ["--gather", "native"]), (4, ["--gather", "native", "--inflight", "1"]),
+                                     (5, ["--gather-batch", "3"]), (6, ["--gather", "native", "--gather-batch", "3"]),
+                                     (7, ["--gather", "ipc"]), (8, ["--gather", "ipc", "--inflight", "1"])])
 def test_bench_dist_path_assembles_the_frame(i, extra):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29611 + i))
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist", "--config", "c2", "--direct", "--steps", "4",
@@ -27,3 +33,19 @@ def test_bench_dist_path_assembles_the_frame(i, extra):
     res = json.loads(line)
     assert res["config"]["gathered_frame_equals_single_rank_render"] is True
     assert res["value"] > 0 and res["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--gather", "ipc", "--pg", "gloo",
+           "--config", "c2", "--direct", "--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--cpu-seconds", "0.5",
+           "--hang-timeout", "100"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == n
+    assert "rt_bands_put" in res["config"]["band_exchange"]
+    assert res["config"]["gathered_frame_equals_single_rank_render"] is True

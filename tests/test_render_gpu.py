@@ -135,6 +135,71 @@ def test_band_tiling_reassembles(renderer, nranks, band_rows):
     assert np.array_equal(img.reshape(-1), full)
 
 
+@pytest.mark.parametrize("nranks,band_rows,w", [(1, 8, 0), (2, 16, 0), (3, 8, 0), (8, 8, 0), (5, 8, 123)])
+def test_band_puts_place_every_rank_into_the_frame(renderer, nranks, band_rows, w):
+    """rt_bands_put (bench.py --gather ipc): each rank's band buffer copied into its rows of
+    the frame by one strided copy (+ one for a short last band) equals a one-rank render;
+    pixels outside the rank's rows are untouched."""
+    import rtamd
+    import torch
+    d = load_golden("hf40k")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w = w or int(d["w"])
+    h = int(d["h"]) - 3  # a short last band
+    full = renderer.render(w, h, depth=1)
+    side = torch.cuda.Stream()
+    frame = torch.full((h * w,), -9, dtype=torch.int32, device="cuda")
+    with torch.cuda.stream(side):
+        s = side.cuda_stream
+        for rank in range(nranks):
+            t = rtamd.rt_tiling(rank, nranks, band_rows, 0)
+            buf = torch.zeros(max(1, rtamd.tiling_pixels(w, h, rank, nranks, band_rows)), dtype=torch.int32,
+                              device="cuda")
+            renderer.render_device(w, h, 1, 0, buf.data_ptr(), tiling=t, stream=s)
+            rtamd.bands_putter(w, h, t)(buf.data_ptr(), frame.data_ptr(), s)
+            torch.cuda.synchronize()
+            got = frame.cpu().numpy().view(np.uint32).reshape(h, w)
+            mine = np.zeros(h, bool)
+            for y0, n in rtamd.rank_bands(h, rank, nranks, band_rows):
+                mine[y0:y0 + n] = True
+            assert np.array_equal(got[mine], full.reshape(h, w)[mine])
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32), full)
+
+
+def test_batched_band_assembly(renderer):
+    """rt_assemble_bands_batch: three frames (different cameras) gathered as one batch per
+    rank re-interleave to the three one-rank renders."""
+    import rtamd
+    import torch
+    d = load_golden("hf40k")
+    renderer.upload(_scene(d))
+    w, h, nranks, R = int(d["w"]), int(d["h"]) - 8, 3, 8
+    cam_params = []
+    for k in range(3):
+        p = np.array(d["params"], np.float32).copy()
+        p[0:3] += 0.01 * k    # nudge the camera basis (rt_params.a)
+        cam_params.append(p)
+    cap = (rtamd.tiling_pixels(w, h, 0, nranks, R) + 3) // 4 * 4
+    side = torch.cuda.Stream()
+    slots = torch.full((nranks, 3, cap), -7, dtype=torch.int32, device="cuda")
+    frames = torch.full((3, h * w), -9, dtype=torch.int32, device="cuda")
+    fulls = []
+    with torch.cuda.stream(side):
+        s = side.cuda_stream
+        for k, p in enumerate(cam_params):
+            renderer.set_params(p)
+            fulls.append(renderer.render(w, h, depth=1))
+            for rank in range(nranks):
+                t = rtamd.rt_tiling(rank, nranks, R, 0)
+                renderer.render_device(w, h, 1, 0, slots[rank, k].data_ptr(), tiling=t, stream=s)
+        rtamd.bands_assembler(w, h, nranks, R, 3 * cap, cap)(frames.data_ptr(), slots.data_ptr(), s, 3)
+    torch.cuda.synchronize()
+    for k in range(3):
+        assert np.array_equal(frames[k].cpu().numpy().view(np.uint32), fulls[k]), k
+    assert not np.array_equal(fulls[0], fulls[2])
+
+
 @pytest.mark.parametrize("nranks,band_rows,w", [(2, 16, 0), (3, 8, 0), (8, 8, 0), (5, 8, 123)])
 def test_device_band_assembly(renderer, nranks, band_rows, w):
     """bench.py's multi-GPU frame path on one device: every rank's bands rendered into
