@@ -50,12 +50,11 @@ def parse_args(argv=None):
     ap.add_argument("--band-rows", type=int, default=8,
                     help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
     ap.add_argument("--dist", action="store_true", help="use the process-group gather path even at N = 1")
-    ap.add_argument("--gather", default="torch", choices=["torch", "native", "ipc"],
-                    help="band exchange at N > 1: torch.distributed gather (async, RCCL) + rt_assemble_bands; "
-                         "native: the library's own RCCL communicator (rt_frame_exchange: gathers in frame order "
-                         "on its stream, rank 0's assembly on another, joined to the render streams by events); "
-                         "ipc: no collective, every rank copies its bands straight into rank 0's frame, mapped "
-                         "through a HIP IPC handle (rt_bands_put)")
+    ap.add_argument("--gather", default="ipc", choices=["ipc", "torch", "native"],
+                    help="band exchange at N > 1.  ipc (default): no collective, every rank copies its bands "
+                         "straight into rank 0's frame, mapped through a HIP IPC handle (rt_bands_put); falls back "
+                         "to torch if any rank cannot map it.  torch: torch.distributed gather (async, RCCL) + "
+                         "rt_assemble_bands.  native: the library's own RCCL communicator (rt_frame_exchange)")
     ap.add_argument("--pg", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for setup and timing; gloo lets a rehearsal run N ranks on one "
                          "GPU (RCCL refuses two ranks on one device)")
@@ -144,16 +143,17 @@ def main():
 
 def run(args, world, result_out=None):
     # Frames in flight run on separate streams; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
-    # queues (4 by default, and exported as 4 on the GPU boxes; shared with torch's and the
-    # library's own streams), so with four frames in flight two would share a queue and
-    # serialise.  Raised to at least 8 before HIP starts (measured: 1/8 shard 0.075 -> 0.055 ms).
-    # Under rocprofv3 the profiler's preload starts HIP first, so the profiling scripts set it
-    # in their own environment; the JSON says which applied.
+    # queues (4 by default, and exported as 4 on the GPU boxes), shared with torch's, RCCL's
+    # and the library's own streams: two frame streams on one queue serialise.  Raised to at
+    # least 16 before HIP starts (measured: 4 -> 8 took a 1/8 shard from 0.075 to 0.055 ms;
+    # with an RCCL process group's streams also in the pool, 8 -> 16 took rank 0's 1/8-shard
+    # frame from 0.071 to 0.045 ms).  Under rocprofv3 the profiler's preload starts HIP first,
+    # so the profiling scripts set it in their own environment; the JSON says which applied.
     q_in = os.environ.get("GPU_MAX_HW_QUEUES")
     hw_queues = {"value": int(q_in) if q_in else 4, "source": "inherited" if q_in else "HIP default"}
-    if hw_queues["value"] < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
-        hw_queues = {"value": 8, "source": "set by bench.py (was %s)" % (q_in or "unset")}
+    if hw_queues["value"] < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+        hw_queues = {"value": 16, "source": "set by bench.py (was %s)" % (q_in or "unset")}
 
     import numpy as np
     import torch

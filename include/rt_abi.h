@@ -223,9 +223,9 @@ int rt_frame_gather(rt_comm* comm, const uint32_t* d_bands, uint64_t slot_pixels
  * with rt_ipc_export (the 64-byte handle of the allocation they lie in + their offset in it)
  * and passes both to the other ranks (any channel), which map the allocation with rt_ipc_open
  * (d_base; the frames are at d_base + offset); then every rank, after rendering a frame's
- * bands, places them into rank 0's frame with rt_bands_put on its own stream: one strided
- * device copy (the rank's bands are evenly spaced in the frame) plus one for a short last
- * band.  Rank 0 puts its own bands the same way into its local frame.  A frame is complete
+ * bands, places them into rank 0's frame with rt_bands_put on its own stream: one copy
+ * kernel, a block per row, writing whole rows (over xGMI for the other ranks).  Rank 0
+ * puts its own bands the same way into its local frame.  A frame is complete
  * when every rank's put has completed (bench.py: device synchronise + barrier).  Replaces
  * the host readback of RayTracer.cpp:343 for a frame rendered on N GPUs. */
 int rt_ipc_export(int32_t device, void* d_ptr, uint8_t* handle, int32_t handle_bytes, uint64_t* offset);

@@ -16,10 +16,10 @@
 //
 // rt_bands_put (bench.py --gather ipc): no collective at all.  Rank 0's framebuffers are
 // exported once as a HIP IPC handle (rt_ipc_alloc / rt_ipc_open); every rank then copies its
-// bands straight to their rows of rank 0's frame with ONE strided copy per frame on its own
-// stream (a rank's bands are evenly spaced: dst pitch = nranks * band).  Over xGMI the copy
-// runs on the sending GPU; rank 0 runs no receive kernel and no re-interleave, and no kernel
-// anywhere spins waiting for a peer.
+// bands straight to their rows of rank 0's frame with one small copy kernel per frame on its
+// own stream (rt_bands_put, rt_render.hip).  Over xGMI the copy runs on the sending GPU; rank
+// 0 runs no receive kernel and no re-interleave, and no kernel anywhere spins waiting for a
+// peer.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
@@ -209,32 +209,6 @@ int rt_ipc_close(int32_t device, void* d_ptr) {
     if (!d_ptr) return RT_ERR_INVALID_ARG;
     (void)hipSetDevice(device);
     return hipIpcCloseMemHandle(d_ptr) == hipSuccess ? RT_OK : comm_err("rt_ipc_close: hipIpcCloseMemHandle", RT_ERR_DEVICE);
-}
-
-int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
-                 void* stream) {
-    if (!d_bands || !d_frame || w == 0 || h == 0) return comm_err("rt_bands_put: invalid argument", RT_ERR_INVALID_ARG);
-    const int32_t N = tiling && tiling->nranks > 1 ? tiling->nranks : 1;
-    const int32_t r = N > 1 ? tiling->rank : 0;
-    const uint32_t R = N > 1 ? (uint32_t)tiling->band_rows : h;
-    if (r < 0 || r >= N || R == 0) return comm_err("rt_bands_put: bad tiling", RT_ERR_INVALID_ARG);
-    hipStream_t st = (hipStream_t)stream;
-    const uint32_t nb = (h + R - 1) / R;                   // bands in the frame; band b = rank b % N
-    const uint32_t mine = nb > (uint32_t)r ? (nb - 1 - r) / N + 1 : 0;
-    if (mine == 0) return RT_OK;
-    const uint32_t last = r + (mine - 1) * N;              // this rank's last band
-    const bool short_last = (uint64_t)(last + 1) * R > h;  // the frame's last band may be short
-    const uint32_t full = mine - (short_last ? 1 : 0);
-    const size_t band_bytes = (size_t)R * w * 4;
-    hipError_t e = hipSuccess;
-    if (full)
-        e = hipMemcpy2DAsync(d_frame + (size_t)r * R * w, band_bytes * N, d_bands, band_bytes, band_bytes, full,
-                             hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess && short_last)
-        e = hipMemcpyAsync(d_frame + (size_t)last * R * w, d_bands + (size_t)full * R * w,
-                           (size_t)(h - last * R) * w * 4, hipMemcpyDeviceToDevice, st);
-    if (e != hipSuccess) return comm_err(std::string("rt_bands_put: ") + hipGetErrorString(e), RT_ERR_DEVICE);
-    return RT_OK;
 }
 
 }  // extern "C"

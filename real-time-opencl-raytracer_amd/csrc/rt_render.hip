@@ -59,7 +59,7 @@ constexpr uint32_t kBlockPx = 16;                    // a block = 2 x 2 tiles of
 
 struct DevScene {
     const float4* __restrict__ wnodes;   // [n_inner][4]
-    const float4* __restrict__ tris;     // [n_refs][3]
+    const float4* __restrict__ tris;     // [n_refs][3] triangle reference records (tri_rec)
     const float4* __restrict__ shade;    // [n_tris][7]
     const int2* __restrict__ leaf_table; // escape leaves {offset, count}
     uint32_t root;
@@ -67,6 +67,10 @@ struct DevScene {
     int fast_div;                        // every box coordinate is 0 or in [2^-66, 2^60]
     int clean;                           // no reachable malformed inner node (kRefError)
 };
+
+// Triangle reference record k (leaf order): {v0.xyz, id}, {e1}, {e2}, 48 B.  (A 40-B
+// record -- two 16-B loads + one 8-B load -- measured 5.6 % slower on C3: DESIGN.md 6.2.)
+__device__ __forceinline__ const float4* tri_rec(const DevScene& S, int k) { return S.tris + (size_t)k * 3; }
 
 struct Frame {
     float3 a, b, c, campos, light_pos, smin, smax;
@@ -412,6 +416,27 @@ __global__ void __launch_bounds__(256) assemble_bands_kernel(uint32_t* __restric
     }
 }
 
+// Band put (rt_bands_put): one block per local row of this rank's band buffer, written to
+// its row of the frame -- a local frame, or rank 0's frame mapped over xGMI (HIP IPC), where
+// whole 16-B-aligned rows make long write bursts.  Pure copy: 8 B/pixel.
+__global__ void __launch_bounds__(256) bands_put_kernel(uint32_t* __restrict__ frame,
+                                                        const uint32_t* __restrict__ bands, uint32_t w,
+                                                        uint32_t local_rows, uint32_t rank, uint32_t nranks,
+                                                        uint32_t band_rows) {
+    const uint32_t lr = blockIdx.x;
+    if (lr >= local_rows) return;
+    const uint64_t y = (uint64_t)(lr / band_rows * nranks + rank) * band_rows + lr % band_rows;
+    const uint32_t* src = bands + (uint64_t)lr * w;
+    uint32_t* dst = frame + y * w;
+    if ((w & 3u) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
 }  // namespace rtk
 
 // Three instantiations of the math + kernels:
@@ -672,6 +697,25 @@ int rt_assemble_bands(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_
     return rt_assemble_bands_batch(d_frame, d_slots, slot_pixels, slot_pixels, 1, w, h, nranks, band_rows, stream);
 }
 
+int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
+                 void* stream) {
+    if (!d_bands || !d_frame || w == 0 || h == 0) return set_err(nullptr, "rt_bands_put: invalid argument", RT_ERR_INVALID_ARG);
+    rt_tiling whole{0, 1, 16, 0};
+    const rt_tiling* T = tiling && tiling->nranks > 1 ? tiling : &whole;
+    if (T->rank < 0 || T->rank >= T->nranks || T->band_rows < 1)
+        return set_err(nullptr, "rt_bands_put: bad tiling", RT_ERR_INVALID_ARG);
+    const int64_t npix = rt_tiling_pixels(w, h, T);
+    if (npix <= 0) return npix < 0 ? set_err(nullptr, "rt_bands_put: bad tiling", RT_ERR_INVALID_ARG) : RT_OK;
+    if ((w & 3u) == 0 && (((uintptr_t)d_frame | (uintptr_t)d_bands) & 15u))
+        return set_err(nullptr, "rt_bands_put: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
+    const uint32_t local_rows = (uint32_t)(npix / w);
+    hipLaunchKernelGGL(rtk::bands_put_kernel, dim3(local_rows), dim3(256), 0, (hipStream_t)stream, d_frame, d_bands, w,
+                       local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(nullptr, std::string("rt_bands_put: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    return RT_OK;
+}
+
 const char* rt_last_error(rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 int rt_create(int device, rt_ctx** out) {
@@ -837,7 +881,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             }
         }
     }
-    // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974)
+    // triangle reference records {v0|id, e1, e2} (volumeRender.cl:965-974), layout of tri_rec
     std::vector<float4> tr((size_t)std::max(nref, 1) * 3 + 1, make_float4(0, 0, 0, 0));
     for (int32_t i = 0; i < nref; ++i) {
         const int32_t tri1 = refs[i];

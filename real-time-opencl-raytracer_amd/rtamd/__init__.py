@@ -677,7 +677,7 @@ def bands_putter(w: int, h: int, tiling: Optional[rt_tiling] = None):
         _stream_arg(stream)
         rc = fn(d_bands, d_frame, *a, stream)
         if rc:
-            raise RtError(rc, lib().rt_comm_last_error().decode())
+            _check(rc)
     return put
 
 

@@ -3,7 +3,7 @@
 # bench.py run, then the median-per-dispatch summary of the render kernel.
 # Usage: scripts/pmc_c3.sh [outdir] ["COUNTER SET 1" "COUNTER SET 2" ...]
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-export GPU_MAX_HW_QUEUES=8
+export GPU_MAX_HW_QUEUES=16
 out=${1:-gpurun_out/pmc}; shift
 if [ $# -eq 0 ]; then
   set -- "GRBM_GUI_ACTIVE TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum" \

@@ -6,7 +6,7 @@
 # Outputs under gpurun_out/prof_*; summarise with scripts/profile_summary.py.
 # Usage: scripts/profile_c3.sh [bench args...]   (default: the C3 headline)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-export GPU_MAX_HW_QUEUES=8
+export GPU_MAX_HW_QUEUES=16
 mkdir -p gpurun_out
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- \
     python3 bench.py --steps 100 --no-cpu-baseline --no-roofline "$@" > gpurun_out/prof_trace.log 2>&1 || exit $?

@@ -1,9 +1,9 @@
 """bench.py's multi-GPU frame path on one GPU, with the assembled frames checked against a
 one-rank render (bench.py's `gathered_frame_equals_single_rank_render`).  Runs bench.py as
 a child process on a small config (C2 scene, 1080p, a few frames):
-  * one rank through every exchange -- the torch.distributed gather (batches of B frames,
-    a part-filled last batch), the library's RCCL communicator (rt_frame_exchange), the
-    IPC band puts (rt_bands_put) -- on a one-rank RCCL process group;
+  * one rank through every exchange -- the IPC band puts (rt_bands_put, the default), the
+    torch.distributed gather (batches of B frames, a part-filled last batch), the library's
+    RCCL communicator (rt_frame_exchange) -- on a one-rank RCCL process group;
   * 2 and 3 ranks sharing the GPU (a gloo process group: RCCL refuses two ranks on one
     device) through the IPC band puts: rank 0's frames mapped into the other processes,
     every rank's bands copied into them -- the driver's N > 1 code path, end to end."""
@@ -21,8 +21,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("i,extra", [(0, []), (1, ["--inflight", "1"]), (2, ["--band-rows", "16"]),
                                      (3, ["--gather", "native"]), (4, ["--gather", "native", "--inflight", "1"]),
-                                     (5, ["--gather-batch", "3"]), (6, ["--gather", "native", "--gather-batch", "3"]),
-                                     (7, ["--gather", "ipc"]), (8, ["--gather", "ipc", "--inflight", "1"])])
+                                     (5, ["--gather", "torch"]), (6, ["--gather", "torch", "--gather-batch", "3"]),
+                                     (7, ["--gather", "native", "--gather-batch", "3"]),
+                                     (8, ["--gather", "torch", "--inflight", "1"])])
 def test_bench_dist_path_assembles_the_frame(i, extra):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29611 + i))
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist", "--config", "c2", "--direct", "--steps", "4",
