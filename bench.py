@@ -641,33 +641,39 @@ def run(args, world, result_out=None):
            "achieved_gbs": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2), "peak_gbs": HBM_PEAK_GBS,
            "note": "SURVEY 8d algorithmic bytes of the reference layout; exceeds HBM peak because the scene is "
                    "served from L1/L2/Infinity Cache"}
-    roof = None
-    if depth == 1 and not args.shard and not args.no_roofline:
+    roof = ft = None
+    if (depth == 1 or wavefront) and not args.shard and not args.no_roofline:
         r.set_params(ptab[0])
-        ft = r.fetch_trace(w, h, flags & ~16)
+        try:
+            ft = r.fetch_counts(w, h, depth, flags & ~16)   # every launch of the frame, counted
+        except rtamd.RtError as e:                           # e.g. a scene off the fast kernel
+            print(f"fetch counts unavailable: {e}", file=sys.stderr)
+            ft = None
+    if ft is not None:
         pk_ms, pk_n = r.gather_peak(16384, 256)          # 1 MiB table: L2-resident on every XCD
         quads = ft["quad_inner"] + ft["quad_tri"]
-        peak_rps = pk_n / (pk_ms * 1e-3)   # every lane a distinct record: one quad request per lane
+        # every lane a distinct record: one quad request per lane; at N > 1 every GPU's path
+        peak_rps = world * pk_n / (pk_ms * 1e-3)
         ach_rps = quads / (ms_per_step * 1e-3)
         roof = {"bound": "l2_gather", "unit": "GB/s",
                 "achieved": round(ach_rps * 64 / 1e9, 2), "peak": round(peak_rps * 64 / 1e9, 2),
                 "frac": round(ach_rps / peak_rps, 4), "traffic": None,
-                "roof": "quad record requests of the traced frame vs random distinct records from an "
-                        "L2-resident table on every CU (rt_gather_peak)",
+                "roof": "quad record requests of the frame (counted on the GPU, every launch) vs random distinct "
+                        "records from an L2-resident table on every CU (rt_gather_peak)"
+                        + (f", x{world} GPUs" if world > 1 else ""),
                 "quad_requests_per_frame": quads, "lane_fetches_per_frame": ft["inner"] + ft["tri"],
                 "lanes_per_quad_request": round((ft["inner"] + ft["tri"]) / max(1, quads), 3),
                 "wave_distinct_records_per_frame": ft["distinct_inner"] + ft["distinct_tri"],
                 "inner_fetches": ft["inner"], "tri_fetches": ft["tri"], "distinct_inner": ft["distinct_inner"],
-                "distinct_tri": ft["distinct_tri"], "wave_instructions": ft["wave_instructions"],
-                "mixed_inner_tri_instructions": ft["mixed_instructions"],
-                "peak_records_per_s": round(peak_rps), "peak_ns_per_record_per_cu": None,
-                "trace_max_iters": ft["max_iters"], "trace_truncated": ft["truncated"]}
+                "distinct_tri": ft["distinct_tri"], "wave_iterations": ft["wave_instructions"],
+                "mixed_inner_tri_iterations": ft["mixed_instructions"],
+                "peak_records_per_s": round(peak_rps), "peak_ns_per_record_per_cu": None}
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        roof["peak_ns_per_record_per_cu"] = round(cus / peak_rps * 1e9, 3)
-    if roof is None:   # wavefront bounces: no replay roof yet; the HBM model of SURVEY 8d
+        roof["peak_ns_per_record_per_cu"] = round(world * cus / peak_rps * 1e9, 3)
+    if roof is None:   # the fused path, or --no-roofline: the HBM model of SURVEY 8d
         roof = {"bound": "hbm", "unit": "GB/s", "achieved": hbm["achieved_gbs"], "peak": HBM_PEAK_GBS,
                 "frac": round(hbm["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
-                "roof": "HBM (the fetch trace covers depth-1 frames only)"}
+                "roof": "HBM (no fetch counts for this run)"}
     roof.update({"hbm": hbm, "stream_copy_gbs": round(stream_copy_gbs, 1), "kernel_ms": round(kernel_ms_avg, 4),
                  "frame_kernels_ms": round(frame_ms_avg, 4), "launches_overlap": F > 1, "kernel": kname,
                  "records_per_ray_oracle": round(rec_inner + rec_tri, 2)})

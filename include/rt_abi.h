@@ -246,26 +246,20 @@ int rt_last_timing(rt_ctx* ctx, float* total_ms, float* traverse_ms);
  * host sync inside its timed loop. */
 int rt_timing_average(rt_ctx* ctx, int32_t n, float* total_ms, float* traverse_ms);
 
-/* Measurement: the traversal's record-fetch stream and its ceiling.
- * rt_trace_frame renders one depth-1 frame (flags as rt_render; whole frame, static block
- * order) with the recording instantiation of the fast kernel: every lane's record fetch,
- * iteration by iteration, goes to d_trace ([waves][cap_iters][64] uint32: bit 31 = triangle
- * record, else inner record; low bits = float4 index; 0xFFFFFFFF = lane idle) and each
- * wave's iteration count to d_wave_len.  trace_bytes >= waves * cap_iters * 256, waves =
- * 4 * ceil(w/16) * ceil(h/16).  The pixel path itself never records (a separate kernel
- * instantiation).
- * rt_trace_stats sums over such a trace: out[0..7] = inner / triangle lane-fetches, inner /
- * triangle QUAD requests (distinct records per quad of lanes per wave instruction: the
- * vector-memory path merges a quad's lanes that read one record), inner / triangle records
- * distinct per wave instruction, wave instructions, and those whose active lanes mix inner
- * and triangle steps.
- * rt_gather_peak measures the ceiling those distinct requests run into: every lane of 8
- * waves per SIMD on every CU reads pseudo-random inner-record-shaped records from a table of
+/* Measurement: the traversal's record fetches and their ceiling.
+ * rt_fetch_counts renders one frame (flags as rt_render; whole frame, static block order;
+ * depth 1, or any depth on the wavefront path: every launch of the frame) with the counting
+ * instantiation of the fast kernels and returns, summed over the frame: out[0..7] = inner /
+ * triangle lane-fetches, inner / triangle QUAD requests (distinct records per quad of lanes
+ * per wave iteration: the vector-memory path merges a quad's lanes that read one record),
+ * inner / triangle records distinct per wave iteration, wave iterations, and those whose
+ * active lanes mix inner and triangle steps.  Traversals restarted with the general code
+ * (stacks deeper than the LDS part; rt_last_deferred) are not counted.  The pixel path itself
+ * never counts (a separate kernel instantiation).
+ * rt_gather_peak measures the ceiling those requests run into: every lane of 8 waves per
+ * SIMD on every CU reads pseudo-random inner-record-shaped records from a table of
  * table_records 64-B records, iters (multiple of 4) per lane: ms per launch and records read. */
-int rt_trace_frame(rt_ctx* ctx, uint32_t w, uint32_t h, uint32_t flags, uint32_t* d_trace, uint64_t trace_bytes,
-                   uint32_t cap_iters, uint32_t* d_wave_len, uint32_t* nwaves);
-int rt_trace_stats(rt_ctx* ctx, const uint32_t* d_trace, const uint32_t* d_wave_len, uint32_t nwaves,
-                   uint32_t cap_iters, uint64_t* out8);
+int rt_fetch_counts(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint64_t* out8);
 int rt_gather_peak(rt_ctx* ctx, uint32_t table_records, uint32_t iters, float* ms, uint64_t* records);
 
 /* Traversals of the last frame that outgrew the fast kernel's LDS stack and

@@ -111,10 +111,8 @@ struct Outputs {
     unsigned long long* overflow;
     uint32_t* restarts;          // traversals that outgrew the LDS stack and restarted (general code)
     uint64_t local_pixels;
-    // measurement instantiation only (rt_trace_frame): per wave [trace_cap][64] record fetches
-    uint32_t* trace;
-    uint32_t* trace_len;         // per wave: iterations recorded
-    uint32_t trace_cap;
+    // measurement instantiation only (rt_fetch_counts): the frame's 8 record-fetch counters
+    unsigned long long* fcount;
 };
 
 __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
@@ -133,9 +131,7 @@ struct Stack {
     uint32_t* lds;      // this lane's column: lds[i * 64]
     uint32_t* glb;      // this pixel's column: glb[(i - kLdsStack) * gstride]
     uint64_t gstride;
-    uint32_t* tr_seg = nullptr;   // fetch trace (measurement instantiation): this wave's segment,
-    uint32_t* tr_it = nullptr;    //   its next free iteration (LDS word),
-    uint32_t tr_cap = 0;          //   and its capacity in iterations
+    uint32_t* fc = nullptr;       // measurement instantiation: this lane's 8 fetch counters (LDS, stride 256)
     __device__ __forceinline__ uint32_t get(int i) const {
         return i < kLdsStack ? lds[i * 64] : glb[(uint64_t)(i - kLdsStack) * gstride];
     }
@@ -144,6 +140,46 @@ struct Stack {
         else glb[(uint64_t)(i - kLdsStack) * gstride] = v;
     }
 };
+
+// Measurement instantiation only (rt_fetch_counts): one traversal iteration's
+// record fetch of every active lane, counted per lane, per quad of lanes and per wave, by
+// record kind; plus the wave's iterations and those that mix inner and triangle fetches.
+// The vector-memory path merges the requests of the lanes of a QUAD (lanes 4k..4k+3) that
+// read the same record (scripts/gather_peak_sweep.py: ~1.2 ns per CU per distinct record per
+// quad, a wave-uniform record ~0.16 ns per lane), so its unit of work is a quad request.
+// fc: this lane's counters [0/1] lane fetches inner/tri, [2/3] quad-distinct, [4/5]
+// wave-distinct, [6] wave iterations, [7] mixed iterations; stride 256 (one block's lanes).
+__device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id) {
+    const uint64_t act = __builtin_amdgcn_read_exec();
+    const int lane = (int)(threadIdx.x & 63u);
+    bool quad_first = true, wave_first = true;
+    for (int j = 0; j < 64; ++j) {   // a lower active lane reading the same record makes this a repeat
+        const uint32_t b = (uint32_t)__shfl((int)id, j);
+        if (j < lane && ((act >> j) & 1ull) && b == id) {
+            wave_first = false;
+            if ((j >> 2) == (lane >> 2)) quad_first = false;
+        }
+    }
+    const uint64_t lm = __builtin_amdgcn_ballot_w64(leaf);
+    const int t = leaf ? 1 : 0;
+    fc[t * 256] += 1u;
+    fc[(2 + t) * 256] += quad_first ? 1u : 0u;
+    fc[(4 + t) * 256] += wave_first ? 1u : 0u;
+    if (lane == (int)__builtin_ctzll(act)) {
+        fc[6 * 256] += 1u;
+        fc[7 * 256] += (lm != 0 && (act & ~lm) != 0) ? 1u : 0u;
+    }
+}
+
+// a block's counters (every thread's 8, stride 256) to the frame's 8 (one thread each)
+__device__ __forceinline__ void fetch_count_flush(const uint32_t* fc_block, unsigned long long* out) {
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        unsigned long long sum = 0;
+        for (int i = 0; i < 256; ++i) sum += fc_block[threadIdx.x * 256 + i];
+        atomicAdd(out + threadIdx.x, sum);
+    }
+}
 
 // local row -> frame row under rt_tiling (bands of band_rows rows, band b -> rank b % nranks)
 __device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
@@ -318,53 +354,6 @@ __global__ void __launch_bounds__(256) wf_scatter_kernel(const uint32_t* __restr
     }
 }
 
-// Fetch-trace statistics (rt_trace_stats): per wave instruction of a traced
-// frame, the lanes that fetched and the distinct records among them.  The vector-memory path
-// merges the requests of the lanes of a QUAD (lanes 4k..4k+3) that read the same record
-// (scripts/gather_peak_sweep.py: a load costs ~1.2 ns per CU per distinct record per quad, a
-// wave-uniform one ~0.16 ns per lane), so the unit of its work is a quad request.
-// Trace entries: bit 31 = triangle record, the rest a float4 index; 0xFFFFFFFF = lane idle.
-// counts: [0] inner lane-fetches, [1] triangle lane-fetches, [2] inner quad requests,
-// [3] triangle quad requests, [4] inner records distinct per wave instruction, [5] the same
-// for triangles, [6] wave instructions (iterations), [7] iterations whose active lanes mix
-// inner and triangle steps (both code paths issue); summed over the frame.
-__global__ void __launch_bounds__(256) trace_stats_kernel(const uint32_t* __restrict__ trace,
-                                                          const uint32_t* __restrict__ len, uint32_t cap,
-                                                          uint32_t nwaves, unsigned long long* __restrict__ counts) {
-    const uint32_t lane = threadIdx.x & 63u, wid = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (wid >= nwaves) return;
-    const uint32_t n = min(len[wid], cap);
-    const uint32_t* seg = trace + (size_t)wid * cap * 64u + lane;
-    uint32_t c[6] = {0, 0, 0, 0, 0, 0}, mixed = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t a = seg[(size_t)i * 64u];
-        const uint64_t tri_lanes = __builtin_amdgcn_ballot_w64(a != 0xFFFFFFFFu && (a >> 31) != 0);
-        const uint64_t inner_lanes = __builtin_amdgcn_ballot_w64(a != 0xFFFFFFFFu && (a >> 31) == 0);
-        mixed += (tri_lanes != 0 && inner_lanes != 0) ? 1u : 0u;
-        bool wave_first = true, quad_first = true;
-        for (int j = 0; j < 64; ++j) {   // a lower lane with the same record makes this one a repeat
-            const uint32_t b = (uint32_t)__shfl((int)a, j);
-            if (j < (int)lane && b == a) {
-                wave_first = false;
-                if ((uint32_t)j >> 2 == lane >> 2) quad_first = false;
-            }
-        }
-        if (a != 0xFFFFFFFFu) {
-            const uint32_t t = a >> 31;
-            c[t] += 1u;
-            c[2 + t] += quad_first ? 1u : 0u;
-            c[4 + t] += wave_first ? 1u : 0u;
-        }
-    }
-    for (int k = 0; k < 6; ++k)
-        for (int o = 32; o > 0; o >>= 1) c[k] += __shfl_xor(c[k], o);
-    if (lane == 0) {
-        for (int k = 0; k < 6; ++k) atomicAdd(counts + k, (unsigned long long)c[k]);
-        atomicAdd(counts + 6, (unsigned long long)n);
-        atomicAdd(counts + 7, (unsigned long long)mixed);
-    }
-}
-
 // Random-record gather ceiling (rt_gather_peak): every lane of every wave
 // reads a different pseudo-random record of the traversal's inner-record shape (three 16-B
 // loads + one 8-B load, 56 of 64 B) from a table of `nrec` 64-B records, `iters` times, four
@@ -523,7 +512,7 @@ struct rt_ctx {
     uint32_t order_tx = 0, order_ty = 0;
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
-    struct { bool on = false; uint32_t* d_trace = nullptr; uint32_t* d_len = nullptr; uint32_t cap = 0; } trace;
+    struct { bool on = false; unsigned long long* d_counts = nullptr; } trace;   // rt_fetch_counts
     bool timing_valid = false;
     std::string err;
 };
@@ -649,7 +638,10 @@ template <int M> struct Kernels;
         static void* bounce(bool fast) {                                                                   \
             return fast ? (void*)NS::wf_bounce_kernel<true> : (void*)NS::wf_bounce_kernel<false>;          \
         }                                                                                                  \
-        static void* traced() { return (void*)NS::first_bounce_kernel<true, false, true>; }               \
+        static void* traced(bool next) {                                                                   \
+            return next ? (void*)NS::first_bounce_kernel<true, true, true> : (void*)NS::first_bounce_kernel<true, false, true>; \
+        }                                                                                                  \
+        static void* traced_bounce() { return (void*)NS::wf_bounce_kernel<true, true>; }                  \
     };
 RTK_KERNELS(0, rtk_strict)
 RTK_KERNELS(1, rtk_hw)
@@ -662,8 +654,11 @@ static void* kernel_first(int m, bool fast, bool next) {
 static void* kernel_fused(int m, bool fast) {
     return m == 0 ? Kernels<0>::fused(fast) : m == 1 ? Kernels<1>::fused(fast) : Kernels<2>::fused(fast);
 }
-static void* kernel_traced(int m) {
-    return m == 0 ? Kernels<0>::traced() : m == 1 ? Kernels<1>::traced() : Kernels<2>::traced();
+static void* kernel_traced(int m, bool next) {
+    return m == 0 ? Kernels<0>::traced(next) : m == 1 ? Kernels<1>::traced(next) : Kernels<2>::traced(next);
+}
+static void* kernel_traced_bounce(int m) {
+    return m == 0 ? Kernels<0>::traced_bounce() : m == 1 ? Kernels<1>::traced_bounce() : Kernels<2>::traced_bounce();
 }
 static void* kernel_bounce(int m, bool fast) {
     return m == 0 ? Kernels<0>::bounce(fast) : m == 1 ? Kernels<1>::bounce(fast) : Kernels<2>::bounce(fast);
@@ -671,7 +666,7 @@ static void* kernel_bounce(int m, bool fast) {
 
 extern "C" {
 
-int rt_abi_version(void) { return 2; }
+int rt_abi_version(void) { return 3; }
 
 int rt_assemble_bands_batch(uint32_t* d_frame, const uint32_t* d_slots, uint64_t slot_pixels, uint64_t frame_pixels,
                             int32_t nframes, uint32_t w, uint32_t h, int32_t nranks, int32_t band_rows, void* stream) {
@@ -1099,9 +1094,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.rgb = aux ? d_aux->rgb : nullptr;
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
-    O.trace = nullptr;
-    O.trace_len = nullptr;
-    O.trace_cap = 0;
+    O.fcount = nullptr;
     const bool traced = c->trace.on;
 
     rt_ctx::FrameEv& E = c->ring[c->frames % rt_ctx::kRing];
@@ -1196,11 +1189,9 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.out_count = cnt + 8 * 1 + 0;
             W.bounce = 0;
             void* args[] = {&S, &F, &O, &W, &ax};
-            if (traced) {   // rt_trace_frame: the recording instantiation of the same kernel
-                O.trace = c->trace.d_trace;
-                O.trace_len = c->trace.d_len;
-                O.trace_cap = c->trace.cap;
-                HIPC(c, hipLaunchKernel(kernel_traced(math), grid, block, args, 0, s));
+            if (traced) {   // rt_fetch_counts: the counting instantiation of the same kernel
+                O.fcount = c->trace.d_counts;
+                HIPC(c, hipLaunchKernel(kernel_traced(math, depth > 1), grid, block, args, 0, s));
             } else {
                 HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
             }
@@ -1233,7 +1224,8 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.fetch = cnt + 8 * k + 2;
             W.bounce = k;
             void* args[] = {&S, &Fb, &O, &W, &ax};
-            HIPC(c, hipLaunchKernel(kernel_bounce(math, fast), dim3(c->wf_grid[math]), dim3(256), args, 0, s));
+            HIPC(c, hipLaunchKernel(traced ? kernel_traced_bounce(math) : kernel_bounce(math, fast), dim3(c->wf_grid[math]),
+                                    dim3(256), args, 0, s));
         }
     }
     HIPC(c, hipGetLastError());
@@ -1322,50 +1314,32 @@ int rt_last_deferred(rt_ctx* c, uint32_t* count) {
     return RT_OK;
 }
 
-int rt_trace_frame(rt_ctx* c, uint32_t w, uint32_t h, uint32_t flags, uint32_t* d_trace, uint64_t trace_bytes,
-                   uint32_t cap_iters, uint32_t* d_wave_len, uint32_t* nwaves) {
-    if (!c || !d_trace || !d_wave_len || !nwaves || cap_iters == 0 || w == 0 || h == 0)
-        return set_err(c, "rt_trace_frame: invalid argument", RT_ERR_INVALID_ARG);
-    if ((flags & (RT_FLAG_WAVEFRONT | RT_FLAG_EXACT_DIV)) || !c->have_scene || !c->clean)
-        return set_err(c, "rt_trace_frame: depth-1 frames of clean scenes on the fast kernel only", RT_ERR_INVALID_ARG);
-    const uint64_t nb = (uint64_t)((w + rtk::kBlockPx - 1) / rtk::kBlockPx) * ((h + rtk::kBlockPx - 1) / rtk::kBlockPx);
-    if (trace_bytes < nb * 4 * cap_iters * 64 * 4)
-        return set_err(c, "rt_trace_frame: trace buffer smaller than waves x cap_iters x 64 x 4 B", RT_ERR_INVALID_ARG);
+int rt_fetch_counts(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint64_t* out8) {
+    if (!c || !out8 || w == 0 || h == 0 || depth < 1 || depth > RT_MAX_DEPTH)
+        return set_err(c, "rt_fetch_counts: invalid argument", RT_ERR_INVALID_ARG);
+    if ((depth > 1 && !(flags & RT_FLAG_WAVEFRONT)) || (flags & RT_FLAG_EXACT_DIV) || !c->have_scene || !c->clean)
+        return set_err(c, "rt_fetch_counts: the fast kernels of a clean scene, depth 1 or the wavefront path",
+                       RT_ERR_INVALID_ARG);
     HIPC(c, hipSetDevice(c->device));
     int rc = ensure(c, c->d_out, c->out_cap, (size_t)w * h);
     if (rc) return rc;
-    HIPC(c, hipMemsetAsync(d_trace, 0xFF, nb * 4 * cap_iters * 64 * 4, c->stream));
-    c->trace.on = true;
-    c->trace.d_trace = d_trace;
-    c->trace.d_len = d_wave_len;
-    c->trace.cap = cap_iters;
-    rc = rt_render_device(c, w, h, 1, flags | RT_FLAG_STATIC_ORDER, nullptr, c->d_out, nullptr, c->stream);
-    c->trace.on = false;
-    if (rc) return rc;
-    HIPC(c, hipStreamSynchronize(c->stream));
-    *nwaves = (uint32_t)(nb * 4);
-    return RT_OK;
-}
-
-int rt_trace_stats(rt_ctx* c, const uint32_t* d_trace, const uint32_t* d_wave_len, uint32_t nwaves, uint32_t cap_iters,
-                   uint64_t* out8) {
-    if (!c || !d_trace || !d_wave_len || nwaves == 0 || cap_iters == 0 || !out8)
-        return set_err(c, "rt_trace_stats: invalid argument", RT_ERR_INVALID_ARG);
-    HIPC(c, hipSetDevice(c->device));
-    unsigned long long* d_counts = nullptr;
-    HIPC(c, hipMalloc((void**)&d_counts, 8 * sizeof(unsigned long long)));
-    hipError_t e = hipMemsetAsync(d_counts, 0, 8 * sizeof(unsigned long long), c->stream);
+    unsigned long long* d = nullptr;
+    HIPC(c, hipMalloc((void**)&d, 8 * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d, 0, 8 * sizeof(unsigned long long), c->stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(rtk::trace_stats_kernel, dim3((nwaves + 3) / 4), dim3(256), 0, c->stream, d_trace, d_wave_len,
-                           cap_iters, nwaves, d_counts);
-        e = hipGetLastError();
+        c->trace.on = true;
+        c->trace.d_counts = d;
+        rc = rt_render_device(c, w, h, depth, flags | RT_FLAG_STATIC_ORDER, nullptr, c->d_out, nullptr, c->stream);
+        c->trace.on = false;
+        c->trace.d_counts = nullptr;
     }
-    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (e == hipSuccess) e = hipMemcpyAsync(h, d_counts, sizeof h, hipMemcpyDeviceToHost, c->stream);
+    unsigned long long hc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (e == hipSuccess && rc == RT_OK) e = hipMemcpyAsync(hc, d, sizeof hc, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(d_counts);
-    if (e != hipSuccess) return set_err(c, std::string("rt_trace_stats: ") + hipGetErrorString(e), RT_ERR_DEVICE);
-    for (int k = 0; k < 8; ++k) out8[k] = h[k];
+    (void)hipFree(d);
+    if (rc) return rc;
+    if (e != hipSuccess) return set_err(c, std::string("rt_fetch_counts: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    for (int k = 0; k < 8; ++k) out8[k] = hc[k];
     return RT_OK;
 }
 

@@ -85,7 +85,7 @@ ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt
                "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
                "rt_frame_ready_wait", "rt_ipc_export", "rt_ipc_open", "rt_ipc_close", "rt_bands_put",
                "rt_scene_image_size", "rt_scene_image_pack",
-               "rt_scene_image_load", "rt_trace_frame", "rt_trace_stats", "rt_gather_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_scene_image_load", "rt_fetch_counts", "rt_gather_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
@@ -136,8 +136,7 @@ def lib() -> C.CDLL:
             "rt_scene_image_size": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
             "rt_scene_image_pack": (C.c_int, [vp, vp, C.c_uint64, vp]),
             "rt_scene_image_load": (C.c_int, [vp, vp, C.c_uint64, vp]),
-            "rt_trace_frame": (C.c_int, [vp, u32, u32, u32, vp, C.c_uint64, u32, vp, C.POINTER(u32)]),
-            "rt_trace_stats": (C.c_int, [vp, vp, vp, u32, u32, C.POINTER(C.c_uint64)]),
+            "rt_fetch_counts": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(C.c_uint64)]),
             "rt_gather_peak": (C.c_int, [vp, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
             "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
@@ -445,25 +444,15 @@ class Renderer:
         self._scene_keepalive = None
         _check(lib().rt_scene_image_load(self._h, C.c_void_p(d_image), nbytes, C.c_void_p(stream or None)), self._h)
 
-    def fetch_trace(self, w: int, h: int, flags: int, cap_iters: int = 1024):
-        """Trace one depth-1 frame's record fetches (rt_trace_frame) and sum them (rt_trace_stats):
-        lane-fetches, quad requests and wave-distinct records (inner / tri), wave instructions."""
-        import torch
-        waves = 4 * ((w + 15) // 16) * ((h + 15) // 16)
-        trace = torch.empty(waves * cap_iters * 64, dtype=torch.int32, device="cuda")
-        wlen = torch.zeros(waves, dtype=torch.int32, device="cuda")
-        nw = C.c_uint32()
-        _check(lib().rt_trace_frame(self._h, w, h, flags, C.c_void_p(trace.data_ptr()), trace.numel() * 4, cap_iters,
-                                    C.c_void_p(wlen.data_ptr()), C.byref(nw)), self._h)
+    def fetch_counts(self, w: int, h: int, depth: int = 1, flags: int = 0):
+        """rt_fetch_counts: one frame's record fetches (every launch of the frame, counting
+        instantiation): lane-fetches, quad requests and wave-distinct records (inner / tri),
+        wave iterations and those mixing inner and triangle steps."""
         out = (C.c_uint64 * 8)()
-        _check(lib().rt_trace_stats(self._h, C.c_void_p(trace.data_ptr()), C.c_void_p(wlen.data_ptr()), nw.value,
-                                    cap_iters, out), self._h)
-        max_it = int(wlen.max().item())
-        del trace, wlen
+        _check(lib().rt_fetch_counts(self._h, w, h, depth, flags, out), self._h)
         return {"inner": int(out[0]), "tri": int(out[1]), "quad_inner": int(out[2]), "quad_tri": int(out[3]),
                 "distinct_inner": int(out[4]), "distinct_tri": int(out[5]), "wave_instructions": int(out[6]),
-                "mixed_instructions": int(out[7]),
-                "max_iters": max_it, "cap_iters": cap_iters, "waves": nw.value, "truncated": max_it > cap_iters}
+                "mixed_instructions": int(out[7])}
 
     def gather_peak(self, table_records: int = 16384, iters: int = 256):
         """rt_gather_peak: (ms per launch, records read) of the random-record gather ceiling."""

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors_without_gpu():
     lib = rtamd.lib()
-    assert lib.rt_abi_version() == 2   # 2: default arithmetic S_ref, RT_FLAG_STRICT_MATH
+    assert lib.rt_abi_version() == 3   # 2: default arithmetic S_ref, RT_FLAG_STRICT_MATH; 3: rt_fetch_counts, IPC puts
     assert lib.rt_set_params(None, None) == -1
     assert lib.rt_render(None, 1, 1, 1, 0, None, None) == -1
     # rt_assemble_bands validates before any device call: null buffers, zero sizes, bad

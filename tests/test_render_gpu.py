@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-4  # north star tolerance on float RGB
 STRICT = 64      # RT_FLAG_STRICT_MATH: the oracle's arithmetic
+WAVEFRONT, WF_SORT = 8, 32   # RT_FLAG_WAVEFRONT, RT_FLAG_WF_SORT
 MODES = {"ref": 0, "strict": STRICT, "hw": 2}   # default S_ref, S_strict, S_hw (RT_FLAG_HW_MATH)
 
 
@@ -449,24 +450,31 @@ def test_scene_image_moves_the_scene_between_contexts(renderer):
 
 
 @pytest.mark.parametrize("name", ["hf40k", "cubes2_dae"])
-def test_fetch_trace_counts_the_oracles_visits(renderer, name):
-    """The recording instantiation behind the roofline (rt_trace_frame + rt_trace_stats): in S_strict
-    its inner-record fetches are exactly the oracle's inner visits (primary + shadow rays, the
-    reference's visit order) and its triangle-record fetches the oracle's triangle tests (plus
-    one per visit of an empty leaf)."""
+def test_fetch_counts_are_the_oracles_visits(renderer, name):
+    """The counting instantiation behind the roofline (rt_fetch_counts): in S_strict its
+    inner-record fetches are exactly the oracle's inner visits (the reference's visit order)
+    and its triangle-record fetches the oracle's triangle tests (plus one per visit of an
+    empty leaf) -- for a depth-1 frame (primary + shadow rays) and for a depth-3 frame on the
+    wavefront path (every bounce launch, primary, shadow and secondary rays)."""
     from oracle import oracle
     d = load_golden(name)
     renderer.upload(_scene(d))
     renderer.set_params(d["params"])
     w, h = int(d["w"]), int(d["h"])
-    fr = renderer.fetch_trace(w, h, STRICT, cap_iters=512)
-    assert not fr["truncated"] and fr["wave_instructions"] > 0
-    assert 0 < fr["distinct_inner"] <= fr["quad_inner"] <= fr["inner"]
-    assert 0 < fr["distinct_tri"] <= fr["quad_tri"] <= fr["tri"]
-    st = oracle.render(d, d["params"], w, h, depth=1, aux=False)["stats"]
-    inner = st["primary"]["inner"] + st["shadow"]["inner"]
-    tris = st["primary"]["tris"] + st["shadow"]["tris"]
-    assert fr["inner"] == inner
-    assert tris <= fr["tri"] <= tris + st["primary"]["leaf"] + st["shadow"]["leaf"]
+    for depth, flags in ((1, STRICT), (3, STRICT | WAVEFRONT), (3, STRICT | WAVEFRONT | WF_SORT)):
+        fr = renderer.fetch_counts(w, h, depth, flags)
+        assert renderer.last_deferred() == 0   # no restarted (uncounted) traversals
+        assert fr["wave_instructions"] > 0 and fr["mixed_instructions"] <= fr["wave_instructions"]
+        assert 0 < fr["distinct_inner"] <= fr["quad_inner"] <= fr["inner"]
+        assert 0 < fr["distinct_tri"] <= fr["quad_tri"] <= fr["tri"]
+        st = oracle.render(d, d["params"], w, h, depth=depth, aux=False)["stats"]
+        kinds = ("primary", "shadow", "secondary")
+        inner = sum(st[k]["inner"] for k in kinds)
+        tris = sum(st[k]["tris"] for k in kinds)
+        leaves = sum(st[k]["leaf"] for k in kinds)
+        assert fr["inner"] == inner, (depth, flags)
+        assert tris <= fr["tri"] <= tris + leaves, (depth, flags)
+    with pytest.raises(Exception):
+        renderer.fetch_counts(w, h, 3, STRICT)   # the fused path has no counting instantiation
     ms, n = renderer.gather_peak(4096, 64)
     assert ms > 0 and n > 0
