@@ -62,6 +62,8 @@ struct DevScene {
     const float4* __restrict__ tris;     // [n_refs][3] triangle reference records (tri_rec)
     const float4* __restrict__ shade;    // [n_tris][7]
     const int2* __restrict__ leaf_table; // escape leaves {offset, count}
+    uint32_t tri_off;                    // byte offset of tris from wnodes (one allocation)
+    uint32_t rec_bytes;                  // bytes of that allocation
     uint32_t root;
     uint32_t n_inner;                    // inner records; the first ones are the BVH's top levels (BFS order)
     int fast_div;                        // every box coordinate is 0 or in [2^-66, 2^60]
@@ -584,9 +586,20 @@ static int slot_for(rt_ctx* c, void* stream, rt_ctx::FrameSlot** out) {
     return RT_OK;
 }
 
+// Inner and triangle records in ONE allocation (triangles right after the inner records),
+// so the fast traversal addresses both with 32-bit offsets from one buffer descriptor.
+static hipError_t alloc_records(rt_ctx* c, size_t n_wnodes4, size_t n_tris4) {
+    if ((n_wnodes4 + n_tris4) * 16 >= 0x80000000ull) return hipErrorInvalidValue;   // 31-bit offsets
+    float4* p = nullptr;
+    const hipError_t e = hipMalloc((void**)&p, (n_wnodes4 + n_tris4) * sizeof(float4));
+    if (e != hipSuccess) return e;
+    c->d_wnodes = p;
+    c->d_tris = p + n_wnodes4;
+    return hipSuccess;
+}
+
 static void free_scene(rt_ctx* c) {
-    if (c->d_wnodes) (void)hipFree(c->d_wnodes);
-    if (c->d_tris) (void)hipFree(c->d_tris);
+    if (c->d_wnodes) (void)hipFree(c->d_wnodes);   // one block: inner records, then triangle records
     if (c->d_shade) (void)hipFree(c->d_shade);
     if (c->d_leaf) (void)hipFree(c->d_leaf);
     if (c->d_rank) (void)hipFree(c->d_rank);
@@ -909,8 +922,7 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
     for (auto& f : c->slots)
         if (f.idle) HIPC(c, hipEventSynchronize(f.idle));   // frames in flight still read the old scene
     free_scene(c);
-    HIPC(c, hipMalloc((void**)&c->d_wnodes, wn.size() * sizeof(float4)));
-    HIPC(c, hipMalloc((void**)&c->d_tris, tr.size() * sizeof(float4)));
+    HIPC(c, alloc_records(c, wn.size(), tr.size()));
     HIPC(c, hipMalloc((void**)&c->d_shade, sh.size() * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_leaf, leaf_table.size() * sizeof(int2)));
     HIPC(c, hipMalloc((void**)&c->d_rank, rank.size() * sizeof(uint32_t)));
@@ -998,8 +1010,7 @@ int rt_scene_image_load(rt_ctx* c, const void* d_image, uint64_t bytes, void* st
     for (auto& f : c->slots)
         if (f.idle) HIPC(c, hipEventSynchronize(f.idle));   // frames in flight still read the old scene
     free_scene(c);
-    HIPC(c, hipMalloc((void**)&c->d_wnodes, h.n_wnodes4 * 16));
-    HIPC(c, hipMalloc((void**)&c->d_tris, h.n_tris4 * 16));
+    HIPC(c, alloc_records(c, h.n_wnodes4, h.n_tris4));
     HIPC(c, hipMalloc((void**)&c->d_shade, std::max<uint64_t>(h.n_shade4, 1) * 16));
     HIPC(c, hipMalloc((void**)&c->d_leaf, h.n_leaf * 8));
     HIPC(c, hipMalloc((void**)&c->d_rank, h.n_rank * 4));
@@ -1085,8 +1096,16 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.tiles_y = (F.local_rows + rtk::kBlockPx - 1) / rtk::kBlockPx;
     F.num_blocks = F.tiles_x * F.tiles_y;
 
-    rtk::DevScene S{c->d_wnodes, c->d_tris, c->d_shade, c->d_leaf, c->root, c->n_inner,
-                    (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0, c->clean};
+    rtk::DevScene S{c->d_wnodes,
+                    c->d_tris,
+                    c->d_shade,
+                    c->d_leaf,
+                    (uint32_t)(c->n_wnodes4 * 16),
+                    (uint32_t)((c->n_wnodes4 + c->n_tris4) * 16),
+                    c->root,
+                    c->n_inner,
+                    (c->fast_div && !(flags & RT_FLAG_EXACT_DIV)) ? 1 : 0,
+                    c->clean};
     rtk::Outputs O;
     O.out = d_out;
     O.hits = aux ? d_aux->hits : nullptr;
