@@ -4,8 +4,10 @@ Product: rt_bvh_build_sbvh (csrc/host/sbvh_builder.cpp, parallel).  Oracle:
 oracle/sbvh_oracle.c, a step-for-step restatement of SplitBVHBuilder.cpp:41-476.
 The reference builder itself does not compile here (pugixml absent), so the
 oracle is pinned by the survey's probe of the real builder on cubes2.obj
-(14,933 nodes, 23,836 tri refs) and by the recorded digest of its
-output (tests/golden/sbvh_digests.json, made by tests/golden/make_sbvh_digests.py).
+(14,933 nodes, 23,836 tri refs; and the traversal work the real tree
+costs per primary ray at 1024x768: 18.74 / 1.60 / 5.98, max stack 14) and by the
+recorded digest of its output (tests/golden/sbvh_digests.json, made by
+tests/golden/make_sbvh_digests.py; a regression lock, not a pin).
 Bar: product bytes == oracle bytes.
 """
 import hashlib
@@ -106,6 +108,27 @@ def test_oracle_pinned_by_survey_probe_on_cubes2():
     assert nodes.shape[0] == 14933 and refs.size == 23836   # SURVEY.md section 6, probe of the real builder
     want = json.load(open(DIGESTS))["cubes2_obj"]
     assert digest(nodes, refs) == want
+
+
+@pytest.mark.skipif(not os.path.exists(CUBES2), reason="reference data not present")
+def test_traversal_work_pinned_by_survey_probe_on_cubes2():
+    """The survey ran the REAL SplitBVHBuilder and the reference's traversal order on cubes2.obj
+    at the reference's 1024x768 with its default camera (SURVEY.md 6 / BASELINE.md: 18.74 inner
+    visits, 1.60 leaves, 5.98 triangle tests per primary ray, max stack depth 14).  The product
+    SBVH traversed by the oracle must do the same work: a structural pin on the tree beyond its
+    node and reference counts (a different split or child order changes these averages)."""
+    from oracle import oracle
+    m = rtamd.Mesh.load_obj(CUBES2)
+    s = rtamd.Scene.from_mesh(m, m.build_sbvh(8))
+    w, h = 1024, 768   # RayTracer.cpp:39-40
+    r = oracle.render(s, rtamd.params_to_array(m.camera_params(w, h)), w, h, depth=1, aux=False)
+    st = r["stats"]
+    pr = st["primary"]
+    assert pr["rays"] == w * h
+    assert round(pr["inner"] / pr["rays"], 2) == 18.74
+    assert round(pr["leaf"] / pr["rays"], 2) == 1.60
+    assert round(pr["tris"] / pr["rays"], 2) == 5.98
+    assert st["max_stack"] == 14
 
 
 def test_recorded_digests_of_synthetic_scenes():
