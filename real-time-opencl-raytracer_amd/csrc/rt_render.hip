@@ -214,18 +214,16 @@ __device__ __forceinline__ void zero_next_counters(const Frame& F) {
 }
 
 // Wave-aggregated append: lanes with `want` get consecutive slots of `q`.
-__device__ __forceinline__ void wf_append(bool want, QRay* q, uint32_t* count, const QRay& r) {
-    const uint64_t m = __builtin_amdgcn_ballot_w64(want);
-    if (!m) return;
+// A queue slot for every active lane of the wave (one atomic per wave; lanes keep their
+// order, so the queue keeps the screen order of the waves that fill it).
+__device__ __forceinline__ QRay* wf_slot(QRay* q, uint32_t* count) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(true);
     const int lane = threadIdx.x & 63;
     const int leader = __builtin_ctzll(m);
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(count, (uint32_t)__builtin_popcountll(m));
     base = __shfl(base, leader);
-    if (want) {
-        const uint32_t slot = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-        q[slot] = r;
-    }
+    return q + base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
 }
 
 // Longest-first block order (LPT list scheduling): the hardware hands blocks to free CU
