@@ -587,7 +587,7 @@ static int slot_for(rt_ctx* c, void* stream, rt_ctx::FrameSlot** out) {
 // Inner and triangle records in ONE allocation (triangles right after the inner records),
 // so the fast traversal addresses both with 32-bit offsets from one buffer descriptor.
 static hipError_t alloc_records(rt_ctx* c, size_t n_wnodes4, size_t n_tris4) {
-    if ((n_wnodes4 + n_tris4) * 16 >= 0x7F000000ull) return hipErrorInvalidValue;   // below rtk kNoRecord
+    if ((n_wnodes4 + n_tris4) * 16 >= 0x80000000ull) return hipErrorInvalidValue;   // 31-bit offsets
     float4* p = nullptr;
     const hipError_t e = hipMalloc((void**)&p, (n_wnodes4 + n_tris4) * sizeof(float4));
     if (e != hipSuccess) return e;
