@@ -710,8 +710,11 @@ def run(args, world, result_out=None):
                    "primary_rays_per_frame": round(prim_total / args.steps, 1),
                    "primary_mrays_per_s": round(prim_total / elapsed / 1e6, 1),
                    "mpixels_per_s": round(w * h * args.steps / elapsed / 1e6, 1),
-                   "parallelism": (f"screen bands x{world} (RCCL gather)" if not args.shard
-                                   else f"shard {args.shard} of the band split (diagnostic, no gather)"),
+                   "parallelism": (f"shard {args.shard} of the band split (diagnostic, no gather)" if args.shard
+                                   else "one rank, whole frame" if not use_dist
+                                   else f"screen bands x{world} ("
+                                        + ("library RCCL gather" if native else "IPC band put" if ipc else "RCCL gather")
+                                        + ")"),
                    "band_rows": args.band_rows, "frames_in_flight": F, "frames_per_gather": B, "buffer_sets": NB,
                    "band_exchange": (None if not use_dist else "rt_frame_exchange (one library RCCL communicator, gather + assembly streams)" if native
                                      else "rt_bands_put: each rank's bands copied straight into rank 0's frame "
