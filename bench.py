@@ -632,9 +632,9 @@ def run(args, world, result_out=None):
     # the vector-memory path (TA/TD), not HBM (nodes and triangles are re-read from L1/L2/Infinity
     # Cache).  That path merges the lanes of a quad that read the same record, and a load costs
     # per distinct record per quad (scripts/gather_peak_sweep.py), so its unit of work is a quad
-    # request.  achieved = the frame's quad requests, counted on the GPU from a trace of this
-    # frame's fetches (rt_trace_frame, a recording instantiation of the same kernel;
-    # rt_trace_stats), over ms_per_step; peak = the measured rate of quad requests when every
+    # request.  achieved = the frame's quad requests, counted on the GPU while rendering this
+    # frame with a counting instantiation of the same kernels (rt_fetch_counts, every launch of
+    # the frame), over ms_per_step; peak = the measured rate of quad requests when every
     # lane reads a different record of an L2-resident table on every CU (rt_gather_peak).
     # Both in 64-B record slots. ----
     hbm = {"bytes_per_ray_reference_layout": round(bpr, 1),
