@@ -151,7 +151,9 @@ struct Stack {
 // quad, a wave-uniform record ~0.16 ns per lane), so its unit of work is a quad request.
 // fc: this lane's counters [0/1] lane fetches inner/tri, [2/3] quad-distinct, [4/5]
 // wave-distinct, [6] wave iterations, [7] mixed iterations; stride 256 (one block's lanes).
-__device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id) {
+// vmem = false: a record the wave read once through the scalar cache (the traversal's
+// wave-uniform prologue): a lane fetch and a wave-distinct record, but no quad request.
+__device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id, bool vmem = true) {
     const uint64_t act = __builtin_amdgcn_read_exec();
     const int lane = (int)(threadIdx.x & 63u);
     bool quad_first = true, wave_first = true;
@@ -165,7 +167,7 @@ __device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id
     const uint64_t lm = __builtin_amdgcn_ballot_w64(leaf);
     const int t = leaf ? 1 : 0;
     fc[t * 256] += 1u;
-    fc[(2 + t) * 256] += quad_first ? 1u : 0u;
+    fc[(2 + t) * 256] += (vmem && quad_first) ? 1u : 0u;
     fc[(4 + t) * 256] += wave_first ? 1u : 0u;
     if (lane == (int)__builtin_ctzll(act)) {
         fc[6 * 256] += 1u;
