@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import datetime
+import glob
 import json
 import os
 import socket
@@ -79,6 +80,20 @@ def parse_args(argv=None):
     ap.add_argument("--extra-flags", type=int, default=0,
                     help="OR-ed into rt_render flags (A/B: 64 = S_strict math, 2 = S_hw math, 4 = division-form "
                          "slab test, 16 = static block order)")
+    ap.add_argument("--warmup-seconds", type=float, default=0.3,
+                    help="after the --warmup frames, keep warming up until this much wall time of frames has run "
+                         "(clock ramp-up after the idle scene setup)")
+    ap.add_argument("--max-extra-warmup", type=int, default=4096, help="cap on the time-based extra warm-up frames")
+    ap.add_argument("--frame-check", default="final", choices=["final", "every"],
+                    help="N > 1 / --dist: final = every frame rank 0 holds at the end is compared with its own "
+                         "one-rank render of that frame's camera; every = also a checksum of every presented frame, "
+                         "taken when rank 0 saw it complete (ipc exchange)")
+    ap.add_argument("--sync-timeout-ms", type=int, default=10000,
+                    help="ipc exchange: bound on a put's wait for its frame set and on rank 0's wait for a frame")
+    ap.add_argument("--inject-fault", default="none", choices=["none", "wrong-bands", "drop-put"],
+                    help="test only (ipc exchange, N > 1): the last rank puts frame 4's bands from another frame's "
+                         "buffer (wrong-bands: the frame check must fail), or skips its put of frame 4 (drop-put: "
+                         "frame delivery must fail by timeout)")
     ap.add_argument("--probe-launch", action="store_true",
                     help="launcher check without a GPU: every rank joins a gloo group and rank 0 reports the world")
     return ap.parse_args(argv)
@@ -110,6 +125,39 @@ def _probe(args):
         print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "all_reduce": float(t.item()),
                           "ranks": ranks}))
     dist.destroy_process_group()
+
+
+def host_cpu_share():
+    """The host cores this process may use: its CPU affinity, capped by the cgroup's CPU quota
+    (a GPU box gives each GPU's job a share of a many-core host: os.cpu_count() reports the
+    whole machine, the quota what the job can actually run on).  OMP_NUM_THREADS is used only
+    when neither is readable."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:   # cgroup v2: "max 100000" or "<quota> <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:   # cgroup v1
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    omp = int(os.environ.get("OMP_NUM_THREADS") or 0) or None
+    if quota is not None:
+        cores, source = max(1, min(affinity, int(quota + 0.5))), "cgroup CPU quota"
+    elif omp is not None and omp < affinity:
+        cores, source = omp, "OMP_NUM_THREADS (no cgroup quota readable)"
+    else:
+        cores, source = affinity, "CPU affinity"
+    return {"cores": cores, "source": source, "affinity": affinity, "cgroup_quota": quota,
+            "omp_num_threads": omp, "os_cpu_count": os.cpu_count()}
 
 
 def _hang_exit(rank, seconds):
@@ -202,7 +250,8 @@ def run(args, world, result_out=None):
     cfg = configs.CONFIGS[args.config]
     w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"] | args.extra_flags
     math_flags = flags & (64 | 2)
-    host_threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    cpu_share = host_cpu_share()
+    host_threads = cpu_share["cores"]
     nframes = args.warmup + args.steps
 
     # ---- scene: rank 0 builds it (Collada round trip + the reference's SBVH) and uploads it;
@@ -317,29 +366,40 @@ def run(args, world, result_out=None):
     gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)] \
         if (use_dist and rank == 0 and not ipc) else None
     glists = [list(g.unbind(0))[:world] for g in gbufs] if gbufs is not None else [None] * NB
-    frames_all = torch.zeros(NB, B, h * w, dtype=torch.int32, device=dev) if (rank == 0 and use_dist) else None
+    # rank 0's frames; on the ipc path followed, in the same allocation, by the frame-sync
+    # block (rt_frame_sync_words) that the ranks' puts and rank 0's presents share
+    nfr_words = NB * B * h * w
+    sync_words = rtamd.frame_sync_words(NB, shard_n) if ipc else 0
+    shared_all = (torch.zeros(nfr_words + (sync_words + 3) // 4 * 4, dtype=torch.int32, device=dev)
+                  if (rank == 0 and use_dist) else None)
+    frames_all = shared_all[:nfr_words].view(NB, B, h * w) if shared_all is not None else None
     frames = list(frames_all) if frames_all is not None else None
     shared = None
+    fsync = None
     if ipc:
-        # rank 0's framebuffers mapped into every rank (rt_ipc_export / rt_ipc_open): each
-        # rank's bands go straight to their rows of rank 0's frame.  If any rank cannot map
-        # them, every rank falls back to the torch.distributed gather.
+        # rank 0's framebuffers (+ sync block) mapped into every rank (rt_ipc_export /
+        # rt_ipc_open): each rank's bands go straight to their rows of rank 0's frame.  Only
+        # where every rank can reach rank 0's GPU (rt_peer_access); otherwise, or if any rank
+        # cannot map them, every rank falls back to the torch.distributed gather.
         store = dist.distributed_c10d._get_default_store()
         ok = 1.0
         try:
             if rank == 0:
                 try:
-                    hnd, off = rtamd.SharedFrames.export(local, frames_all.data_ptr())
-                    store.set("rtamd_ipc", hnd + off.to_bytes(8, "little"))
+                    hnd, off = rtamd.SharedFrames.export(local, shared_all.data_ptr())
+                    store.set("rtamd_ipc", hnd + off.to_bytes(8, "little") + local.to_bytes(4, "little"))
                 except rtamd.RtError:
                     store.set("rtamd_ipc", b"")
                     raise
-                fr_base = frames_all.data_ptr()
+                fr_base = shared_all.data_ptr()
             else:
                 blob = bytes(store.get("rtamd_ipc"))
-                if len(blob) != rtamd.SharedFrames.HANDLE_BYTES + 8:
+                if len(blob) != rtamd.SharedFrames.HANDLE_BYTES + 12:
                     raise rtamd.RtError(-2, "rank 0 could not export its frames")
-                shared = rtamd.SharedFrames.open(local, blob[:-8], int.from_bytes(blob[-8:], "little"))
+                dev0 = int.from_bytes(blob[-4:], "little")
+                if not rtamd.peer_access(local, dev0):
+                    raise rtamd.RtError(-2, f"device {local} cannot access rank 0's device {dev0} (no peer access)")
+                shared = rtamd.SharedFrames.open(local, blob[:-12], int.from_bytes(blob[-12:-4], "little"))
                 fr_base = shared.ptr
         except rtamd.RtError as e:
             print(f"rank {rank}: frame mapping unavailable ({e}); using torch.distributed", file=sys.stderr)
@@ -355,8 +415,19 @@ def run(args, world, result_out=None):
                 gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)]
                 glists = [list(g.unbind(0))[:world] for g in gbufs]
         else:
-            put = rtamd.bands_putter(w, h, tiling)
             put_dst = [[fr_base + 4 * (j * B + s) * h * w for s in range(B)] for j in range(NB)]
+            sync_local = torch.zeros(NB, dtype=torch.int32, device=dev)   # this rank's per-set block counters
+            fsync = rtamd.FrameSync(w, h, tiling, shard_n, NB, fr_base + 4 * nfr_words, sync_local.data_ptr(),
+                                    args.sync_timeout_ms)
+            use = [0] * NB   # times set j has been filled
+    # frame checks: the camera index of every frame a set last held, and (--frame-check
+    # every, rank 0) each presented frame's checksum, taken on its stream right after the
+    # present saw it complete
+    frame_of = [[-1] * B for _ in range(NB)]
+    fault = args.inject_fault != "none" and rank == world - 1 and world > 1
+    check_every = use_dist and rank == 0 and args.frame_check == "every"
+    sums = torch.zeros(nframes + args.max_extra_warmup, dtype=torch.int64, device=dev) if check_every else None
+    sums_ptr = sums.data_ptr() if sums is not None else 0
 
     # rays traced by this rank in a frame with params p (counted with the aux planes, untimed)
     d = max(depth, 1)
@@ -413,9 +484,22 @@ def run(args, world, result_out=None):
     def exchange(j, k, nfr):
         """Set j's batch (nfr frames, rendered on stream k = the current stream) to rank 0."""
         filled[j] = nfr
-        if ipc:      # this rank's bands into their rows of rank 0's frame, after the render
+        if ipc:      # this rank's bands into their rows of rank 0's frame, after the render;
+            # rank 0 then waits (on this stream) until every rank's rows of the frame are in
             for s in range(nfr):
-                put(out_ptr[j][s], put_dst[j][s], sh[k])
+                src = out_ptr[j][s]
+                if fault and frame_of[j][s] == 4:
+                    if args.inject_fault == "drop-put":
+                        use[j] += 1
+                        continue
+                    src = out_ptr[(j + 1) % NB][s]   # another frame's bands
+                fsync.put(j, use[j], src, put_dst[j][s], sh[k])
+                if rank == 0:   # the set goes back to the ranks after its consumer (the checksum)
+                    fsync.present(j, use[j], sh[k], release=not check_every)
+                    if check_every:
+                        rtamd.frame_checksum(put_dst[j][s], h * w, sums_ptr + 8 * frame_of[j][s], sh[k])
+                        fsync.release(j, use[j], sh[k])
+                use[j] += 1
             return
         if native:   # gather on the rt_comm's stream after the renders, rank 0's assembly after it
             xchg(j, nfr, outs_ptr[j], slots_ptr[j], fr_ptr[j], sh[k])
@@ -447,8 +531,9 @@ def run(args, world, result_out=None):
             elif native:                 # likewise, through the rt_comm's events
                 slot_wait(j, sh[k])
         if orbit_params is not None:   # updateCamera (RayTracer.cpp:609-672) for this frame
-            set_params(hdl, orbit_params[n])
+            set_params(hdl, orbit_params[n % len(orbit_params)])
         launch(out_ptr[j][s], sh[k])
+        frame_of[j][s] = n
         s += 1
         if s < B:
             cur[1] = s
@@ -466,9 +551,34 @@ def run(args, world, result_out=None):
             exchange(b % NB, b % F, s)
         cur[0], cur[1] = b + (1 if s else 0), 0
 
+    # Warm-up: the --warmup frames, then more until --warmup-seconds of frames have run (the
+    # GPU's clocks ramp up over a fraction of a second after the idle scene setup: 20 frames
+    # measured right after 5 warm-up frames ran 10 % slower than in steady state).  Every rank
+    # warms up as many frames as the slowest-to-warm rank (agreed through an all-reduce, so the
+    # ranks' frame sequences stay in step).
     for _ in range(args.warmup):
         step()
     drain()
+    torch.cuda.synchronize(dev)
+    tw = time.perf_counter()
+    extra = 0
+    while args.warmup_seconds > 0 and extra < args.max_extra_warmup:
+        chunk = min(64, args.max_extra_warmup - extra)
+        for _ in range(chunk):
+            step()
+        drain()
+        torch.cuda.synchronize(dev)
+        extra += chunk
+        if time.perf_counter() - tw >= args.warmup_seconds:
+            break
+    if use_dist:   # every rank runs the largest extra warm-up of any rank
+        ex = torch.tensor([float(extra)], device=dev)
+        allreduce(ex, dist.ReduceOp.MAX)
+        for _ in range(int(ex.item()) - extra):
+            step()
+        extra = int(ex.item())
+        drain()
+    warmup_frames = args.warmup + extra
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -489,11 +599,15 @@ def run(args, world, result_out=None):
     # records on the launch stream around each frame's kernels (ring of 64 frames)
     frame_ms_avg, kernel_ms_avg = r.timing_average(min(args.steps, 64))
 
+    total_frames = warmup_frames + args.steps
+    # frame n was rendered with camera n % L (the orbit table wraps when the time-based
+    # warm-up ran past it; a static camera has L = 1)
+    L = ptab.shape[0]
     # rays of the timed frames (untimed: one aux render per distinct camera)
     if args.orbit:
         rays_local = prim_local = 0
-        for p in ptab[args.warmup:]:
-            a, b = count_rays(p)
+        for n in range(warmup_frames, total_frames):
+            a, b = count_rays(ptab[n % L])
             rays_local += a
             prim_local += b
         r.set_params(ptab[0])
@@ -501,14 +615,50 @@ def run(args, world, result_out=None):
         rays_local, prim_local = rays_f0 * args.steps, prim_f0 * args.steps
     del hits, tt, rgb
 
-    # check (untimed): rank 0's assembled frames equal its own one-rank render of the frame
+    # Frame delivery (ipc): rank 0 observed every frame complete (rt_frame_present), or the run
+    # failed.  `value` counts only presented frames.
+    sync_info = None
+    if fsync is not None and rank == 0:
+        st, presented = fsync.status()
+        sync_info = {"status": st, "frames_presented": presented, "frames_rendered": total_frames}
+        if st != 0 or presented != total_frames:
+            raise SystemExit(f"bench.py: frame delivery failed: {sync_info} (1 = a put timed out waiting for "
+                             "its frame set, 2 = rank 0 timed out waiting for the ranks' rows)")
+
+    # check (untimed): every frame rank 0 holds at the end (and, with --frame-check every, the
+    # checksum every presented frame had when rank 0 saw it complete) equals rank 0's own
+    # one-rank render of that frame's camera.  Under --orbit every frame differs, so a band
+    # landing in the wrong frame, or overwriting a frame before it was presented, is caught.
     frame_ok = None
-    if use_dist and rank == 0 and not args.orbit and not args.shard:
+    frame_check = None
+    if use_dist and rank == 0 and not args.shard:
         full = torch.zeros(h * w, dtype=torch.int32, device=dev)
-        r.render_device(w, h, depth, flags, full.data_ptr(), stream=streams[0].cuda_stream)
-        torch.cuda.synchronize(dev)
-        frame_ok = sum(filled) > 0 and all(bool(torch.equal(full, frames[j][s]))
-                                           for j in range(NB) for s in range(filled[j]))
+        ref_sum = torch.zeros(1, dtype=torch.int64, device=dev)
+        sum_of = {}
+
+        def reference(cam):   # rank 0's one-rank frame of camera index cam into `full`; its checksum
+            r.set_params(ptab[cam])
+            r.render_device(w, h, depth, flags, full.data_ptr(), stream=streams[0].cuda_stream)
+            ref_sum.zero_()
+            rtamd.frame_checksum(full.data_ptr(), h * w, ref_sum.data_ptr(), streams[0].cuda_stream)
+            torch.cuda.synchronize(dev)
+            sum_of[cam] = int(ref_sum.item())
+            return sum_of[cam]
+
+        held = [(j, s) for j in range(NB) for s in range(filled[j]) if frame_of[j][s] >= 0]
+        frame_ok = bool(held)
+        for j, s in held:
+            reference(frame_of[j][s] % L)
+            frame_ok = frame_ok and bool(torch.equal(full, frames[j][s]))
+        frame_check = {"held_frames_checked": len(held), "held_frames_equal": frame_ok,
+                       "distinct_cameras": min(L, total_frames)}
+        if check_every and sums is not None:
+            got = sums[:total_frames].cpu().numpy()
+            bad = [n for n in range(total_frames) if int(got[n]) != sum_of.get(n % L, None) and
+                   int(got[n]) != reference(n % L)]
+            frame_check.update({"presented_frames_checksummed": total_frames, "checksum_mismatches": len(bad)})
+            frame_ok = frame_ok and not bad
+        r.set_params(ptab[0])
 
     # (untimed for `value`) the reference's own boundary: rt_render, synchronous, the frame
     # read back into host memory (raytrace_gpgpu: launch + clFinish + clEnqueueReadBuffer,
@@ -595,8 +745,10 @@ def run(args, world, result_out=None):
     if world == 1 and not args.no_cpu_baseline:
         cpu = {"value": cpu_rays * reps / cpu_s / 1e6, "unit": "Mrays/s", "cores": ncores, "kind": "port",
                "sample": f"oracle/rt_oracle.c on every {stride}th pixel of the same frame ({npix_sample} px, "
-                         f"{cpu_rays} rays) x {reps} repetition(s), {cpu_s:.1f} s, {ncores} threads "
-                         f"(the box's CPU share; os.cpu_count() = {os.cpu_count()})"}
+                         f"{cpu_rays} rays) x {reps} repetition(s), {cpu_s:.1f} s, {ncores} threads = every "
+                         f"core this job may use ({cpu_share['source']}: affinity {cpu_share['affinity']} CPUs, "
+                         f"cgroup quota {cpu_share['cgroup_quota']}, os.cpu_count() {cpu_share['os_cpu_count']})",
+               "host_cpu_share": cpu_share}
         if stride == 1:
             # the oracle's frame against the GPU's frame in the oracle's arithmetic (S_strict),
             # whole frame, same camera; the benched arithmetic is pinned to the reference
@@ -642,13 +794,21 @@ def run(args, world, result_out=None):
            "note": "SURVEY 8d algorithmic bytes of the reference layout; exceeds HBM peak because the scene is "
                    "served from L1/L2/Infinity Cache"}
     roof = ft = None
+    fetch_cams = [0]
     if (depth == 1 or wavefront) and not args.shard and not args.no_roofline:
-        r.set_params(ptab[0])
+        # the timed frames' cameras (orbit: up to 8 spread over the timed frames, averaged)
+        timed = sorted({n % L for n in range(warmup_frames, total_frames)})
+        fetch_cams = [timed[i * len(timed) // min(8, len(timed))] for i in range(min(8, len(timed)))]
         try:
-            ft = r.fetch_counts(w, h, depth, flags & ~16)   # every launch of the frame, counted
+            fts = []
+            for cam in fetch_cams:
+                r.set_params(ptab[cam])
+                fts.append(r.fetch_counts(w, h, depth, flags & ~16))   # every launch of the frame, counted
+            ft = {k: sum(f[k] for f in fts) / len(fts) for k in fts[0]}
         except rtamd.RtError as e:                           # e.g. a scene off the fast kernel
             print(f"fetch counts unavailable: {e}", file=sys.stderr)
             ft = None
+        r.set_params(ptab[0])
     if ft is not None:
         pk_ms, pk_n = r.gather_peak(16384, 256)          # 1 MiB table: L2-resident on every XCD
         quads = ft["quad_inner"] + ft["quad_tri"]
@@ -667,7 +827,8 @@ def run(args, world, result_out=None):
                 "inner_fetches": ft["inner"], "tri_fetches": ft["tri"], "distinct_inner": ft["distinct_inner"],
                 "distinct_tri": ft["distinct_tri"], "wave_iterations": ft["wave_instructions"],
                 "mixed_inner_tri_iterations": ft["mixed_instructions"],
-                "peak_records_per_s": round(peak_rps), "peak_ns_per_record_per_cu": None}
+                "peak_records_per_s": round(peak_rps), "peak_ns_per_record_per_cu": None,
+                "fetch_counts_cameras": len(fetch_cams)}
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         roof["peak_ns_per_record_per_cu"] = round(world * cus / peak_rps * 1e9, 3)
     if roof is None:   # the fused path, or --no-roofline: the HBM model of SURVEY 8d
@@ -677,13 +838,21 @@ def run(args, world, result_out=None):
     roof.update({"hbm": hbm, "stream_copy_gbs": round(stream_copy_gbs, 1), "kernel_ms": round(kernel_ms_avg, 4),
                  "frame_kernels_ms": round(frame_ms_avg, 4), "launches_overlap": F > 1, "kernel": kname,
                  "records_per_ray_oracle": round(rec_inner + rec_tri, 2)})
-    pmc = os.path.join(ROOT, "profiles", "r02", f"pmc_{args.config}.json")
-    if os.path.exists(pmc) and not args.orbit and not args.extra_flags:
+    # HBM traffic: PMC counters need rocprofv3, so they come from separate profiling runs of this
+    # command (scripts/pmc_c3.sh); the newest round's file is used and labelled as such, with the
+    # library build it measured -- stale if that is not the library this run loaded
+    pmc_files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{args.config}.json")))
+    if pmc_files and not args.orbit and not args.extra_flags:
         try:
-            pj = json.load(open(pmc))
+            pj = json.load(open(pmc_files[-1]))
+            lib_now = rtamd.library_digest()
             roof["traffic"] = pj.get("hbm_bytes_per_launch")
-            roof["traffic_source"] = (f"profiles/r02/pmc_{args.config}.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                                      "passes of this command (separate runs), FETCH_SIZE x2 per the guide")
+            roof["traffic_source"] = {
+                "file": os.path.relpath(pmc_files[-1], ROOT),
+                "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command (separate runs, not this "
+                       "process), FETCH_SIZE x2 per the guide",
+                "library_measured": pj.get("library_digest"), "library_now": lib_now,
+                "stale": pj.get("library_digest") != lib_now}
         except (OSError, ValueError):
             pass
 
@@ -694,6 +863,7 @@ def run(args, world, result_out=None):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_frames_run": warmup_frames,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
         "scaling": "strong",
@@ -737,6 +907,12 @@ def run(args, world, result_out=None):
         res["parity_vs_oracle"] = parity
     if frame_ok is not None:
         res["config"]["gathered_frame_equals_single_rank_render"] = frame_ok
+        res["config"]["frame_check"] = frame_check
+    if sync_info is not None:
+        res["config"]["frame_delivery"] = dict(sync_info, protocol=(
+            "rt_bands_put_sync + rt_frame_present: every rank publishes its rows of each frame with a system-scope "
+            "release; rank 0's stream waits for all ranks' rows of every frame before the frame counts, and a set is "
+            "refilled only after rank 0 has presented (and consumed) its previous frame"))
     if host_boundary is not None:
         res["config"]["host_boundary"] = host_boundary
     print(json.dumps(res), file=result_out or sys.stdout, flush=True)

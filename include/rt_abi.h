@@ -225,14 +225,48 @@ int rt_frame_gather(rt_comm* comm, const uint32_t* d_bands, uint64_t slot_pixels
  * (d_base; the frames are at d_base + offset); then every rank, after rendering a frame's
  * bands, places them into rank 0's frame with rt_bands_put on its own stream: one copy
  * kernel, a block per row, writing whole rows (over xGMI for the other ranks).  Rank 0
- * puts its own bands the same way into its local frame.  A frame is complete
- * when every rank's put has completed (bench.py: device synchronise + barrier).  Replaces
+ * puts its own bands the same way into its local frame.  rt_bands_put itself carries no
+ * completion signal; the frame path uses rt_bands_put_sync + rt_frame_present below, which
+ * tell rank 0 when each frame is complete.  Replaces
  * the host readback of RayTracer.cpp:343 for a frame rendered on N GPUs. */
 int rt_ipc_export(int32_t device, void* d_ptr, uint8_t* handle, int32_t handle_bytes, uint64_t* offset);
 int rt_ipc_open(int32_t device, const uint8_t* handle, int32_t handle_bytes, void** d_base);
 int rt_ipc_close(int32_t device, void* d_base);
 int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
                  void* stream);
+/* Whether `device` can map `peer`'s memory (hipDeviceCanAccessPeer; 1 for device == peer).
+ * bench.py maps rank 0's frames only when every rank can; otherwise it uses the RCCL gather. */
+int rt_peer_access(int32_t device, int32_t peer, int32_t* can);
+
+/* Per-frame completion of the band puts.  The reference hands back a complete frame every
+ * frame: clFinish + blocking read (RayTracer.cpp:340-343).  Here rank 0 keeps a sync block of
+ * rt_frame_sync_words(nsets, nranks) uint32 words next to its frames (zeroed once, mapped into
+ * every rank with them); frame buffer sets 0..nsets-1 are reused in turn, `use` counting the
+ * times a set has been filled (0, 1, 2, ...).  Per frame:
+ *   every rank: rt_bands_put_sync(..., d_sync, d_local, nsets, set, use, timeout, stream) --
+ *     first waits until rank 0 has presented the set's previous use (no rank ever overwrites
+ *     a frame rank 0 has not observed complete), then copies its rows (as rt_bands_put), then
+ *     publishes "use done" for this rank with a system-scope release; d_local = nsets uint32
+ *     counters in the rank's own memory, zeroed once;
+ *   rank 0, after its own put: rt_frame_present(d_sync, nsets, set, use, nranks, timeout,
+ *     release, stream) -- one wave that waits for every rank's publication of (set, use),
+ *     acquires and counts the frame as presented.  Work enqueued on `stream` after it sees
+ *     the complete frame.  With release != 0 it also hands the set back to the ranks for its
+ *     next use; otherwise rank 0 calls rt_frame_release(d_sync, nsets, set, use, stream)
+ *     after the frame's consumers (a display copy, a checksum) on that stream.
+ * Waits are bounded (timeout_ms, 0 = 10 s); a timeout sets a status instead of hanging:
+ * rt_frame_sync_status reads it (0 ok, 1 a put timed out, 2 a present timed out) and the
+ * number of frames presented (synchronous).  rt_frame_checksum adds a position-dependent
+ * 64-bit sum of a frame's pixels into *d_sum (frame checks). */
+int64_t rt_frame_sync_words(int32_t nsets, int32_t nranks);
+int rt_bands_put_sync(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
+                      uint32_t* d_sync, uint32_t* d_local, int32_t nsets, int32_t set, uint32_t use, uint32_t timeout_ms,
+                      void* stream);
+int rt_frame_present(uint32_t* d_sync, int32_t nsets, int32_t set, uint32_t use, int32_t nranks, uint32_t timeout_ms,
+                     int32_t release, void* stream);
+int rt_frame_release(uint32_t* d_sync, int32_t nsets, int32_t set, uint32_t use, void* stream);
+int rt_frame_sync_status(const uint32_t* d_sync, uint32_t* status, uint32_t* presented);
+int rt_frame_checksum(const uint32_t* d_frame, uint64_t pixels, uint64_t* d_sum, void* stream);
 
 /* Kernel-side timing of the last render, from HIP events on the launch stream
  * (ms): total_ms = every kernel of the frame (counter reset / block-order

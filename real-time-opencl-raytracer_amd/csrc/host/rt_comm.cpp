@@ -205,6 +205,20 @@ int rt_ipc_open(int32_t device, const uint8_t* handle, int32_t handle_bytes, voi
     return RT_OK;
 }
 
+int rt_peer_access(int32_t device, int32_t peer, int32_t* can) {
+    if (!can) return comm_err("rt_peer_access: invalid argument", RT_ERR_INVALID_ARG);
+    *can = 0;
+    if (device == peer) {   // the same GPU: its own memory
+        *can = 1;
+        return RT_OK;
+    }
+    int v = 0;
+    const hipError_t e = hipDeviceCanAccessPeer(&v, device, peer);
+    if (e != hipSuccess) return comm_err(std::string("rt_peer_access: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    *can = v ? 1 : 0;
+    return RT_OK;
+}
+
 int rt_ipc_close(int32_t device, void* d_ptr) {
     if (!d_ptr) return RT_ERR_INVALID_ARG;
     (void)hipSetDevice(device);

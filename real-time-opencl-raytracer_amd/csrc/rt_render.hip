@@ -428,6 +428,118 @@ __global__ void __launch_bounds__(256) bands_put_kernel(uint32_t* __restrict__ f
     }
 }
 
+// ---- per-frame completion of the band puts (rt_bands_put_sync / rt_frame_present) ----
+// The sync block lives in rank 0's memory, mapped into every rank with the frames:
+//   [0] status (0 ok, 1 a put timed out waiting for its set, 2 a present timed out waiting
+//   for the puts), [1] frames presented, [2 .. 2+nsets) release[set] (uses of the set rank 0
+//   has presented), then arrive[set][rank] (uses of the set whose rows the rank has put).
+// Every wait is bounded (s_memrealtime, 100 MHz): a lost peer ends in a status, never a hang.
+constexpr uint32_t kSyncHead = 2;
+__device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// rt_bands_put_sync: one block per local row.  Before writing set `set` for its use `use`
+// the block waits until rank 0 has presented the set's previous use (back-pressure: a peer
+// never overwrites a frame rank 0 has not yet observed complete).  After its row, every
+// block releases its stores at system scope (each XCD's L2 written back) and counts itself
+// on this rank's own counter for the set; the block that completes the count publishes
+// arrive[set][rank] = use + 1 with a system-scope release store.
+__global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restrict__ frame,
+                                                             const uint32_t* __restrict__ bands, uint32_t w,
+                                                             uint32_t local_rows, uint32_t rank, uint32_t nranks,
+                                                             uint32_t band_rows, uint32_t* sync, uint32_t* local,
+                                                             uint32_t nsets, uint32_t set, uint32_t use,
+                                                             uint64_t timeout_ticks) {
+    __shared__ uint32_t s_abort;
+    const uint32_t lr = blockIdx.x;
+    if (threadIdx.x == 0) {
+        uint32_t ab = 0;
+        if (use > 0) {
+            const uint64_t t0 = now_ticks();
+            while (sys_load(sync + kSyncHead + set) < use) {
+                if (now_ticks() - t0 > timeout_ticks) {
+                    __hip_atomic_store(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ab = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        s_abort = ab;
+    }
+    __syncthreads();
+    if (s_abort) return;   // the set's arrival is never published: rank 0's present times out too
+    const uint64_t y = (uint64_t)(lr / band_rows * nranks + rank) * band_rows + lr % band_rows;
+    const uint32_t* src = bands + (uint64_t)lr * w;
+    uint32_t* dst = frame + y * w;
+    if ((w & 3u) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) dst[i] = src[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: this block's row is out of every cache
+        const uint32_t prev = __hip_atomic_fetch_add(local + set, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1u == (use + 1u) * local_rows) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(sync + kSyncHead + nsets + set * nranks + rank, use + 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// rt_frame_present (rank 0, one wave): waits until every rank has published its rows of
+// use `use` of set `set`, acquires them (system scope) and counts the frame as presented;
+// with `release`, also releases the set for its next use (else rt_frame_release does, after
+// the caller's consumers of the frame).
+__global__ void __launch_bounds__(64) frame_present_kernel(uint32_t* sync, uint32_t nsets, uint32_t set, uint32_t use,
+                                                           uint32_t nranks, uint64_t timeout_ticks, uint32_t release) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t0 = now_ticks();
+    bool ok = true;
+    for (uint32_t r = lane; r < nranks; r += 64) {
+        while (sys_load(sync + kSyncHead + nsets + set * nranks + r) < use + 1u) {
+            if (now_ticks() - t0 > timeout_ticks) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    const bool all_ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+    if (lane == 0) {
+        if (!all_ok) {
+            __hip_atomic_store(sync, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (release) __hip_atomic_store(sync + kSyncHead + set, use + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// rt_frame_release: rank 0 is done with use `use` of set `set`; the ranks may refill it.
+__global__ void __launch_bounds__(64) frame_release_kernel(uint32_t* sync, uint32_t set, uint32_t use) {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // the frame's readers are done (stream order)
+        __hip_atomic_store(sync + kSyncHead + set, use + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// rt_frame_checksum: a position-dependent 64-bit sum of a frame (a pixel in the wrong row,
+// or a row from another frame, changes it), added into sums[index].
+__global__ void __launch_bounds__(256) frame_checksum_kernel(const uint32_t* __restrict__ frame, uint64_t pixels,
+                                                             unsigned long long* __restrict__ sums) {
+    unsigned long long acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < pixels; i += (uint64_t)gridDim.x * 256u)
+        acc += (((unsigned long long)frame[i] << 32) | (i & 0xFFFFFFFFull)) * 0x9E3779B97F4A7C15ull;
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o);
+    if ((threadIdx.x & 63u) == 0) atomicAdd(sums, acc);
+}
+
 }  // namespace rtk
 
 // Three instantiations of the math + kernels:
@@ -721,6 +833,75 @@ int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_
                        local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(nullptr, std::string("rt_bands_put: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    return RT_OK;
+}
+
+int64_t rt_frame_sync_words(int32_t nsets, int32_t nranks) {
+    if (nsets < 1 || nranks < 1) return -1;
+    return (int64_t)rtk::kSyncHead + nsets + (int64_t)nsets * nranks;
+}
+
+static uint64_t timeout_ticks(uint32_t ms) { return (uint64_t)(ms ? ms : 10000u) * 100000ull; }   // s_memrealtime: 100 MHz
+
+int rt_bands_put_sync(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
+                      uint32_t* d_sync, uint32_t* d_local, int32_t nsets, int32_t set, uint32_t use, uint32_t timeout_ms,
+                      void* stream) {
+    if (!d_bands || !d_frame || !d_sync || !d_local || w == 0 || h == 0 || nsets < 1 || set < 0 || set >= nsets)
+        return set_err(nullptr, "rt_bands_put_sync: invalid argument", RT_ERR_INVALID_ARG);
+    rt_tiling whole{0, 1, 16, 0};
+    const rt_tiling* T = tiling && tiling->nranks > 1 ? tiling : &whole;
+    if (T->rank < 0 || T->rank >= T->nranks || T->band_rows < 1)
+        return set_err(nullptr, "rt_bands_put_sync: bad tiling", RT_ERR_INVALID_ARG);
+    const int64_t npix = rt_tiling_pixels(w, h, T);
+    if (npix <= 0) return set_err(nullptr, "rt_bands_put_sync: this rank owns no rows", RT_ERR_INVALID_ARG);
+    if ((w & 3u) == 0 && (((uintptr_t)d_frame | (uintptr_t)d_bands) & 15u))
+        return set_err(nullptr, "rt_bands_put_sync: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
+    const uint32_t local_rows = (uint32_t)(npix / w);
+    hipLaunchKernelGGL(rtk::bands_put_sync_kernel, dim3(local_rows), dim3(256), 0, (hipStream_t)stream, d_frame, d_bands,
+                       w, local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows, d_sync, d_local,
+                       (uint32_t)nsets, (uint32_t)set, use, timeout_ticks(timeout_ms));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(nullptr, std::string("rt_bands_put_sync: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    return RT_OK;
+}
+
+int rt_frame_present(uint32_t* d_sync, int32_t nsets, int32_t set, uint32_t use, int32_t nranks, uint32_t timeout_ms,
+                     int32_t release, void* stream) {
+    if (!d_sync || nsets < 1 || set < 0 || set >= nsets || nranks < 1)
+        return set_err(nullptr, "rt_frame_present: invalid argument", RT_ERR_INVALID_ARG);
+    hipLaunchKernelGGL(rtk::frame_present_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_sync, (uint32_t)nsets,
+                       (uint32_t)set, use, (uint32_t)nranks, timeout_ticks(timeout_ms), release ? 1u : 0u);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(nullptr, std::string("rt_frame_present: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    return RT_OK;
+}
+
+int rt_frame_release(uint32_t* d_sync, int32_t nsets, int32_t set, uint32_t use, void* stream) {
+    if (!d_sync || nsets < 1 || set < 0 || set >= nsets)
+        return set_err(nullptr, "rt_frame_release: invalid argument", RT_ERR_INVALID_ARG);
+    hipLaunchKernelGGL(rtk::frame_release_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_sync, (uint32_t)set, use);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(nullptr, std::string("rt_frame_release: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    return RT_OK;
+}
+
+int rt_frame_sync_status(const uint32_t* d_sync, uint32_t* status, uint32_t* presented) {
+    if (!d_sync || !status || !presented) return set_err(nullptr, "rt_frame_sync_status: invalid argument", RT_ERR_INVALID_ARG);
+    uint32_t v[2] = {0, 0};
+    hipError_t e = hipMemcpy(v, d_sync, sizeof v, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return set_err(nullptr, std::string("rt_frame_sync_status: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    *status = v[0];
+    *presented = v[1];
+    return RT_OK;
+}
+
+int rt_frame_checksum(const uint32_t* d_frame, uint64_t pixels, uint64_t* d_sum, void* stream) {
+    if (!d_frame || !d_sum || pixels == 0) return set_err(nullptr, "rt_frame_checksum: invalid argument", RT_ERR_INVALID_ARG);
+    const uint64_t blocks = std::min<uint64_t>(1024, (pixels + 255) / 256);
+    hipLaunchKernelGGL(rtk::frame_checksum_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, d_frame,
+                       pixels, (unsigned long long*)d_sum);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(nullptr, std::string("rt_frame_checksum: ") + hipGetErrorString(e), RT_ERR_DEVICE);
     return RT_OK;
 }
 

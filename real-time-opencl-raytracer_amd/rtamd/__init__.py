@@ -84,6 +84,8 @@ ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt
                "rt_tiling_pixels", "rt_assemble_bands", "rt_assemble_bands_batch", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
                "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
                "rt_frame_ready_wait", "rt_ipc_export", "rt_ipc_open", "rt_ipc_close", "rt_bands_put",
+               "rt_peer_access", "rt_frame_sync_words", "rt_bands_put_sync", "rt_frame_present", "rt_frame_release",
+               "rt_frame_sync_status", "rt_frame_checksum",
                "rt_scene_image_size", "rt_scene_image_pack",
                "rt_scene_image_load", "rt_fetch_counts", "rt_gather_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
@@ -132,6 +134,13 @@ def lib() -> C.CDLL:
             "rt_ipc_open": (C.c_int, [i32, vp, i32, C.POINTER(vp)]),
             "rt_ipc_close": (C.c_int, [i32, vp]),
             "rt_bands_put": (C.c_int, [vp, vp, u32, u32, vp, vp]),
+            "rt_peer_access": (C.c_int, [i32, i32, C.POINTER(i32)]),
+            "rt_frame_sync_words": (C.c_int64, [i32, i32]),
+            "rt_bands_put_sync": (C.c_int, [vp, vp, u32, u32, vp, vp, vp, i32, i32, u32, u32, vp]),
+            "rt_frame_present": (C.c_int, [vp, i32, i32, u32, i32, u32, i32, vp]),
+            "rt_frame_release": (C.c_int, [vp, i32, i32, u32, vp]),
+            "rt_frame_sync_status": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32)]),
+            "rt_frame_checksum": (C.c_int, [vp, C.c_uint64, vp, vp]),
             "rt_frame_ready_wait": (C.c_int, [vp, i32, vp]),
             "rt_scene_image_size": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
             "rt_scene_image_pack": (C.c_int, [vp, vp, C.c_uint64, vp]),
@@ -176,6 +185,14 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def library_digest() -> str:
+    """sha256 (first 16 hex digits) of the librtamd.so this process loads: ties a profile
+    taken in a separate run to the exact kernels it measured."""
+    import hashlib
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -668,6 +685,66 @@ def bands_putter(w: int, h: int, tiling: Optional[rt_tiling] = None):
         if rc:
             _check(rc)
     return put
+
+
+def peer_access(device: int, peer: int) -> bool:
+    """rt_peer_access: can `device` map `peer`'s memory (hipDeviceCanAccessPeer)."""
+    v = C.c_int32()
+    rc = lib().rt_peer_access(device, peer, C.byref(v))
+    if rc:
+        raise RtError(rc, lib().rt_comm_last_error().decode())
+    return bool(v.value)
+
+
+def frame_sync_words(nsets: int, nranks: int) -> int:
+    return int(lib().rt_frame_sync_words(nsets, nranks))
+
+
+class FrameSync:
+    """Per-frame completion of the IPC band puts (rt_bands_put_sync / rt_frame_present).
+    d_sync: rank 0's sync block (mapped on the other ranks), d_local: this rank's nsets
+    counters; both zeroed by the caller before first use.  put(set, use, d_bands, d_frame,
+    stream) every rank; present(set, use, stream) rank 0 after its own put (release(set, use,
+    stream) after its consumers, when present was told not to release)."""
+
+    def __init__(self, w: int, h: int, tiling: Optional[rt_tiling], nranks: int, nsets: int, d_sync: int,
+                 d_local: int, timeout_ms: int = 0):
+        L = lib()
+        self._put, self._present = L.rt_bands_put_sync, L.rt_frame_present
+        self._tl = None if tiling is None else C.byref(tiling)
+        self._wh = (C.c_uint32(w), C.c_uint32(h))
+        self.nranks, self.nsets, self.timeout = nranks, nsets, timeout_ms
+        self.d_sync, self.d_local = d_sync, d_local
+
+    def put(self, set_: int, use: int, d_bands: int, d_frame: int, stream: int) -> None:
+        _stream_arg(stream)
+        rc = self._put(d_bands, d_frame, *self._wh, self._tl, self.d_sync, self.d_local, self.nsets, set_, use,
+                       self.timeout, stream)
+        if rc:
+            _check(rc)
+
+    def present(self, set_: int, use: int, stream: int, release: bool = True) -> None:
+        _stream_arg(stream)
+        rc = self._present(self.d_sync, self.nsets, set_, use, self.nranks, self.timeout, 1 if release else 0, stream)
+        if rc:
+            _check(rc)
+
+    def release(self, set_: int, use: int, stream: int) -> None:
+        """rt_frame_release: after the frame's consumers on `stream` (present(..., release=False))."""
+        _stream_arg(stream)
+        _check(lib().rt_frame_release(self.d_sync, self.nsets, set_, use, stream))
+
+    def status(self):
+        """(status, frames presented): 0 = ok, 1 = a put timed out, 2 = a present timed out."""
+        st, n = C.c_uint32(), C.c_uint32()
+        _check(lib().rt_frame_sync_status(self.d_sync, C.byref(st), C.byref(n)))
+        return st.value, n.value
+
+
+def frame_checksum(d_frame: int, pixels: int, d_sum: int, stream: int) -> None:
+    """rt_frame_checksum: add the frame's position-dependent 64-bit sum into *d_sum."""
+    _stream_arg(stream)
+    _check(lib().rt_frame_checksum(d_frame, pixels, d_sum, stream))
 
 
 def _stream_arg(stream):

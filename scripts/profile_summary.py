@@ -8,6 +8,7 @@ MI355X_MICROARCH.md HBM section); FETCH_SIZE / WRITE_SIZE are in kB = 1024 B.
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import shutil
@@ -70,6 +71,10 @@ def main():
                       "kB = 1024 B",
         "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --config " + cfg,
+        # the library these passes ran (the profiled tree's lib/librtamd.so; bench.py marks the
+        # traffic stale when it loads a different one)
+        "library_digest": hashlib.sha256(open(os.path.join(ROOT, "real-time-opencl-raytracer_amd", "lib",
+                                                             "librtamd.so"), "rb").read()).hexdigest()[:16],
     }
     json.dump(res, open(os.path.join(out, f"pmc_{cfg}.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -6,7 +6,9 @@ a child process on a small config (C2 scene, 1080p, a few frames):
     RCCL communicator (rt_frame_exchange) -- on a one-rank RCCL process group;
   * 2 and 3 ranks sharing the GPU (a gloo process group: RCCL refuses two ranks on one
     device) through the IPC band puts: rank 0's frames mapped into the other processes,
-    every rank's bands copied into them -- the driver's N > 1 code path, end to end."""
+    every rank's bands copied into them, every frame's completion observed by rank 0 --
+    the driver's N > 1 code path, end to end, on an orbiting camera, with injected faults
+    that the frame check and the delivery protocol must catch."""
 import json
 import os
 import subprocess
@@ -36,17 +38,47 @@ def test_bench_dist_path_assembles_the_frame(i, extra):
     assert res["value"] > 0 and res["n_gpus"] == 1
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
+def _ranks_on_one_gpu(n, extra, timeout=115):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--gather", "ipc", "--pg", "gloo",
-           "--config", "c2", "--direct", "--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--cpu-seconds", "0.5",
-           "--hang-timeout", "100"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
+           "--config", "c2", "--direct", "--warmup", "2", "--warmup-seconds", "0", "--no-cpu-baseline",
+           "--cpu-seconds", "0.5", "--hang-timeout", "100"] + extra
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
+    """Every frame differs (orbiting camera); rank 0 observes each frame complete
+    (rt_frame_present), checksums it right then, and every checksum and every frame it holds at
+    the end equal its own one-rank render of that frame's camera."""
+    p = _ranks_on_one_gpu(n, ["--steps", "24", "--orbit", "0.01", "--frame-check", "every"])
     assert p.returncode == 0, p.stderr[-2000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
     assert res["n_gpus"] == n
     assert "rt_bands_put" in res["config"]["band_exchange"]
+    fd, fc = res["config"]["frame_delivery"], res["config"]["frame_check"]
+    assert fd["status"] == 0 and fd["frames_presented"] == fd["frames_rendered"] == 26
+    assert fc["presented_frames_checksummed"] == 26 and fc["checksum_mismatches"] == 0
+    assert fc["held_frames_checked"] == 8 and fc["distinct_cameras"] == 26
     assert res["config"]["gathered_frame_equals_single_rank_render"] is True
+
+
+def test_frame_check_catches_a_band_from_another_frame():
+    """The last rank puts frame 4's bands from another frame's buffer: the per-frame checksum
+    (orbiting camera: every frame differs) must flag exactly that frame."""
+    p = _ranks_on_one_gpu(2, ["--steps", "10", "--orbit", "0.01", "--frame-check", "every",
+                              "--inject-fault", "wrong-bands"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["config"]["frame_check"]["checksum_mismatches"] == 1
+    assert res["config"]["gathered_frame_equals_single_rank_render"] is False
+
+
+def test_frame_delivery_fails_when_a_rank_drops_a_frame():
+    """The last rank never puts frame 4: rank 0's present of that frame times out (bounded wait)
+    and bench.py fails instead of counting the frame."""
+    p = _ranks_on_one_gpu(2, ["--steps", "6", "--sync-timeout-ms", "300", "--inject-fault", "drop-put"])
+    assert p.returncode != 0
+    assert "frame delivery failed" in p.stderr
