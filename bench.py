@@ -94,6 +94,9 @@ def parse_args(argv=None):
                     help="test only (ipc exchange, N > 1): the last rank puts frame 4's bands from another frame's "
                          "buffer (wrong-bands: the frame check must fail), or skips its put of frame 4 (drop-put: "
                          "frame delivery must fail by timeout)")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="raise GPU_MAX_HW_QUEUES to at least this before HIP starts (frames in flight need a "
+                         "hardware queue each, beside torch's and RCCL's streams); 0 = keep the inherited value")
     ap.add_argument("--probe-launch", action="store_true",
                     help="launcher check without a GPU: every rank joins a gloo group and rank 0 reports the world")
     return ap.parse_args(argv)
@@ -197,11 +200,13 @@ def run(args, world, result_out=None):
     # with an RCCL process group's streams also in the pool, 8 -> 16 took rank 0's 1/8-shard
     # frame from 0.071 to 0.045 ms).  Under rocprofv3 the profiler's preload starts HIP first,
     # so the profiling scripts set it in their own environment; the JSON says which applied.
+    # --hw-queues 0 keeps the inherited value; the JSON reports both.
     q_in = os.environ.get("GPU_MAX_HW_QUEUES")
-    hw_queues = {"value": int(q_in) if q_in else 4, "source": "inherited" if q_in else "HIP default"}
-    if hw_queues["value"] < 16:
-        os.environ["GPU_MAX_HW_QUEUES"] = "16"
-        hw_queues = {"value": 16, "source": "set by bench.py (was %s)" % (q_in or "unset")}
+    inherited = int(q_in) if q_in else 4
+    hw_queues = {"inherited": q_in or "unset (HIP default 4)", "effective": inherited, "set_by_bench": False}
+    if args.hw_queues and inherited < args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
+        hw_queues.update(effective=args.hw_queues, set_by_bench=True)
 
     import numpy as np
     import torch

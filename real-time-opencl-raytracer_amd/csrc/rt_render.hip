@@ -245,8 +245,10 @@ __device__ __forceinline__ uint32_t lpt_key(uint32_t c) {
 // launch of its own.  Inter-workgroup hand-off (MI355X_MICROARCH.md, visibility table
 // row 1): one lane per block stores its cost write-through (sc1), waits for the store,
 // then adds to one agent-scope counter; the block whose add returns num_blocks - 1 is
-// last, acquires, and reads every cost with sc1 loads.  `scratch` is >= 772 words of
-// LDS that no wave uses any more (the traversal stacks).
+// last, acquires, and reads every cost with sc1 loads.  `scratch` is >= kEpilogueWords
+// words of LDS that no wave uses any more (the traversal stacks).
+constexpr int kEpilogueWords = 8 + 256 + 2 * 256;   // wave times + flag, histogram, two scan rows
+static_assert(4 * kLdsStack * 64 >= kEpilogueWords, "tile_epilogue's scratch must fit the blocks' traversal stacks");
 __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uint32_t* scratch) {
     if (!F.tile_cost) return;   // launch-uniform
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -590,6 +592,7 @@ struct rt_ctx {
     uint32_t rank_shift = 0;   // wavefront sort keys: leaf positions >> rank_shift fit 13 bits
     int fast_div = 0;
     int clean = 0;
+    bool split_records = false;   // records >= 2 GiB: two allocations, general traversal only
     bool have_scene = false;
     bool have_params = false;
     rt_params params{};
@@ -700,8 +703,25 @@ static int slot_for(rt_ctx* c, void* stream, rt_ctx::FrameSlot** out) {
 
 // Inner and triangle records in ONE allocation (triangles right after the inner records),
 // so the fast traversal addresses both with 32-bit offsets from one buffer descriptor.
+// Buffer-load offsets are 31-bit: records of 2 GiB or more (roughly 25 M triangle
+// references) get two allocations instead, and such a scene renders with the general
+// traversal (pointer loads, any size).  RTAMD_RECORD_LIMIT (bytes) lowers that limit for
+// tests.
+static uint64_t record_limit() {
+    const char* v = std::getenv("RTAMD_RECORD_LIMIT");
+    const uint64_t lim = v ? std::strtoull(v, nullptr, 10) : 0;
+    return lim && lim < 0x80000000ull ? lim : 0x80000000ull;
+}
+
 static hipError_t alloc_records(rt_ctx* c, size_t n_wnodes4, size_t n_tris4) {
-    if ((n_wnodes4 + n_tris4) * 16 >= 0x80000000ull) return hipErrorInvalidValue;   // 31-bit offsets
+    c->split_records = (n_wnodes4 + n_tris4) * 16 >= record_limit();
+    if (c->split_records) {
+        hipError_t e = hipMalloc((void**)&c->d_wnodes, n_wnodes4 * sizeof(float4));
+        if (e != hipSuccess) { c->d_wnodes = nullptr; return e; }
+        e = hipMalloc((void**)&c->d_tris, n_tris4 * sizeof(float4));
+        if (e != hipSuccess) c->d_tris = nullptr;
+        return e;
+    }
     float4* p = nullptr;
     const hipError_t e = hipMalloc((void**)&p, (n_wnodes4 + n_tris4) * sizeof(float4));
     if (e != hipSuccess) return e;
@@ -711,7 +731,8 @@ static hipError_t alloc_records(rt_ctx* c, size_t n_wnodes4, size_t n_tris4) {
 }
 
 static void free_scene(rt_ctx* c) {
-    if (c->d_wnodes) (void)hipFree(c->d_wnodes);   // one block: inner records, then triangle records
+    if (c->split_records && c->d_tris) (void)hipFree(c->d_tris);
+    if (c->d_wnodes) (void)hipFree(c->d_wnodes);   // (one block: inner records, then triangle records)
     if (c->d_shade) (void)hipFree(c->d_shade);
     if (c->d_leaf) (void)hipFree(c->d_leaf);
     if (c->d_rank) (void)hipFree(c->d_rank);
@@ -1357,14 +1378,20 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         F.lpt_next = L.d_lpt;
         F.done = L.d_done;
     }
-    const bool fast = S.clean != 0;   // any quotient domain: traverse_fast picks the variant
+    // the fast kernels (any quotient domain: traverse_fast picks the variant) need a clean scene
+    // whose records one buffer descriptor covers
+    const bool fast = S.clean != 0 && !c->split_records;
     const dim3 grid(F.num_blocks), block(256);
     int ax = aux ? 1 : 0;
     HIPC(c, hipEventRecord(E.e[0], s));
 
+    // The frame's first kernel zeroes the other parity set for the next frame: from then on
+    // the next frame on this slot must use that set, even if a later launch of this frame
+    // fails (its set's queue counts and cursors are then stale).
     if (!wavefront) {
         void* args[] = {&S, &F, &O, &ax};
         HIPC(c, hipLaunchKernel(kernel_fused(math, fast), grid, block, args, 0, s));
+        ++L.nframe;
     } else {
         // Wavefront: bounce 0 over tiles, then one persistent launch per further bounce
         // over the queue of rays still in flight.
@@ -1395,6 +1422,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             } else {
                 HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
             }
+            ++L.nframe;
         }
         if (depth > 1) {
             HIPC(c, hipEventRecord(E.e[2], s));
@@ -1432,7 +1460,6 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     HIPC(c, hipEventRecord(E.e[1], s));
     HIPC(c, hipEventRecord(L.idle, s));
     if (F.tile_cost) L.cost_ready = true;
-    ++L.nframe;
     c->timing_valid = true;
     ++c->frames;
     return RT_OK;
@@ -1517,7 +1544,8 @@ int rt_last_deferred(rt_ctx* c, uint32_t* count) {
 int rt_fetch_counts(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint64_t* out8) {
     if (!c || !out8 || w == 0 || h == 0 || depth < 1 || depth > RT_MAX_DEPTH)
         return set_err(c, "rt_fetch_counts: invalid argument", RT_ERR_INVALID_ARG);
-    if ((depth > 1 && !(flags & RT_FLAG_WAVEFRONT)) || (flags & RT_FLAG_EXACT_DIV) || !c->have_scene || !c->clean)
+    if ((depth > 1 && !(flags & RT_FLAG_WAVEFRONT)) || (flags & RT_FLAG_EXACT_DIV) || !c->have_scene || !c->clean ||
+        c->split_records)
         return set_err(c, "rt_fetch_counts: the fast kernels of a clean scene, depth 1 or the wavefront path",
                        RT_ERR_INVALID_ARG);
     HIPC(c, hipSetDevice(c->device));

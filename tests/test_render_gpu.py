@@ -478,3 +478,43 @@ def test_fetch_counts_are_the_oracles_visits(renderer, name):
         renderer.fetch_counts(w, h, 3, STRICT)   # the fused path has no counting instantiation
     ms, n = renderer.gather_peak(4096, 64)
     assert ms > 0 and n > 0
+
+
+@pytest.mark.parametrize("name", ["knot16k", "rand4k_sbvh"])
+def test_records_beyond_the_buffer_load_limit_render_with_the_general_traversal(renderer, name, monkeypatch):
+    """Scenes whose inner + triangle records reach the 31-bit buffer-load limit (2 GiB, about
+    25 M triangle references) get two allocations and render with the general traversal.
+    RTAMD_RECORD_LIMIT lowers the limit so a fixture takes that path: same bits as the oracle,
+    in every mode, on the fused and wavefront paths, and through a scene image."""
+    import rtamd
+    d = load_golden(name)
+    w, h = int(d["w"]), int(d["h"])
+    ref = _oracle(d, 3)
+    normal = {}
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    for m, f in MODES.items():
+        normal[m] = renderer.render(w, h, depth=3, flags=f)
+    monkeypatch.setenv("RTAMD_RECORD_LIMIT", "1024")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    _compare(renderer.render(w, h, depth=3, flags=STRICT, aux=True), ref, f"{name} split records")
+    for m, f in MODES.items():
+        assert np.array_equal(renderer.render(w, h, depth=3, flags=f), normal[m]), m
+        assert np.array_equal(renderer.render(w, h, depth=3, flags=f | WAVEFRONT), normal[m]), m
+    with pytest.raises(rtamd.RtError):   # the counting kernels are fast-path only
+        renderer.fetch_counts(w, h, 1, 0)
+    # moved through a scene image into a second context (which allocates split records too)
+    import torch
+    nb = renderer.scene_image_size()
+    img = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    renderer.pack_scene(img.data_ptr(), nb)
+    r2 = rtamd.Renderer(0)
+    try:
+        r2.load_scene(img.data_ptr(), nb)
+        r2.set_params(d["params"])
+        assert np.array_equal(r2.render(w, h, depth=3, flags=0), normal["ref"])
+    finally:
+        r2.close()
+    monkeypatch.delenv("RTAMD_RECORD_LIMIT")
+    renderer.upload(_scene(d))   # back to one allocation for the tests that follow
