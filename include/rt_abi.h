@@ -84,8 +84,10 @@ enum {
                                 launch per further bounce over a compacted queue of the rays still in
                                 flight, instead of the fused one-lane-per-pixel kernel; bit-identical.
                                 Depth-1 frames always run as that first launch alone. */
-    RT_FLAG_WF_SORT = 32u,   /* with RT_FLAG_WAVEFRONT: sort each bounce's queue by (direction octant,
-                                leaf position of the triangle the ray leaves) before tracing it */
+    RT_FLAG_WF_SORT = 32u,   /* with RT_FLAG_WAVEFRONT: sort each bounce's queue before tracing it, within
+                                screen-local chunks of 1024 rays, by the direction component along the scene
+                                box's thinnest axis (8 buckets; stable), so that rays of similar length share
+                                waves; pixels are identical either way */
     RT_FLAG_EXACT_DIV = 4u,  /* force the division form of the slab test (volumeRender.cl:614-615) instead
                                 of the bit-identical fast quotient; for A/B only */
     RT_FLAG_STATIC_ORDER = 16u /* keep the static XCD-dealt block order instead of the adaptive

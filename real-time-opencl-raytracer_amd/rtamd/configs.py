@@ -5,9 +5,8 @@ C1: the 12-triangle Cornell room at 256x256, depth 1 (the reference's CPU-path c
 C2: a 70,144-tri torus knot at 1080p, primary rays only.
 C3: a 1M-tri value-noise heightfield at 1080p, primary + 1 shadow ray (the metric's config).
 C4: the C3 scene at 4K (the multi-GPU scaling curve).
-C5: 10 x C3 on a 5x2 grid = 10M tris at 1080p, depth 3, wavefront mode; the bounce queues stay in
-    the order the compaction produces (tile order: rays grouped by origin), which measured faster
-    than an explicit per-bounce sort by hit node (c5s: the same with RT_FLAG_WF_SORT).
+C5: 10 x C3 on a 5x2 grid = 10M tris at 1080p, depth 3, wavefront mode with per-bounce ray
+    sorting (c5u: unsorted, for A/B).
 """
 from __future__ import annotations
 
@@ -38,17 +37,18 @@ CONFIGS = {
     "c4": dict(scene="heightfield", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=HF_EXT, w=3840, h=2160, depth=1,
                flags=0, desc="C4: C3 scene at 3840x2160, primary + 1 shadow ray"),
     # configs[4]: 10M tris (10 x C3 on a 5x2 grid), depth 3 (primary + 2 bounces, shadows), in
-    # the wavefront mode: per-bounce compacted queues, kept in the tile order the compaction
-    # produces (an explicit per-bounce sort by hit node measured slower: c5s)
+    # the wavefront mode with per-bounce ray sorting: each bounce queue is reordered within
+    # screen-local chunks of 1024 rays by the rays' direction along the scene's thinnest axis
+    # (rt_render.hip wf_local_sort_kernel)
     "c5": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920,
-               h=1080, depth=3, flags=RT_FLAG_WAVEFRONT,
+               h=1080, depth=3, flags=RT_FLAG_WAVEFRONT | RT_FLAG_WF_SORT,
                dae=False,  # a 1 GB Collada text file is not worth the round trip; built in memory
                desc="C5: 10M-tri merged scene (10 x C3 on a 5x2 grid), 1920x1080, 3 bounces with shadows, "
-                    "wavefront mode (per-bounce compacted ray queues in tile order)"),
-    # the same with the explicit per-bounce counting sort by (hit-node leaf position, octant)
-    "c5s": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920,
-                h=1080, depth=3, flags=RT_FLAG_WAVEFRONT | RT_FLAG_WF_SORT, dae=False,
-                desc="C5 scene and frame, wavefront mode with per-bounce ray sorting by hit node"),
+                    "wavefront mode with per-bounce ray sorting (screen-local chunks, by direction)"),
+    # A/B: the same without the sort (queues in the compaction's tile order)
+    "c5u": dict(scene="hf10", nx=500, nz=1000, amp=10.0, seed=0x5EED, ext=(-80.0, 80.0, -200.0, 200.0), w=1920,
+                h=1080, depth=3, flags=RT_FLAG_WAVEFRONT, dae=False,
+                desc="C5 scene and frame, wavefront mode, bounce queues unsorted (tile order)"),
 }
 
 

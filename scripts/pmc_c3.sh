@@ -1,7 +1,7 @@
 #!/bin/bash
 # Separate rocprofv3 --pmc passes (counters only, no trace domains) over a short
 # bench.py run, then the median-per-dispatch summary of the render kernel.
-# Usage: scripts/pmc_c3.sh [outdir] ["COUNTER SET 1" "COUNTER SET 2" ...]
+# Usage: [BENCH_ARGS="--config c5"] scripts/pmc_c3.sh [outdir] ["COUNTER SET 1" "COUNTER SET 2" ...]
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 export GPU_MAX_HW_QUEUES=16
 out=${1:-gpurun_out/pmc}; shift
@@ -18,6 +18,6 @@ i=0
 for set in "$@"; do
   i=$((i+1))
   timeout -k 10 180 rocprofv3 --pmc $set -d $out/p$i -o run --output-format csv -- \
-      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-roofline --inflight 1 > $out/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+      python3 bench.py --steps 5 --warmup 1 --warmup-seconds 0 --no-cpu-baseline --no-roofline --inflight 1 $BENCH_ARGS > $out/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
 python3 scripts/pmc_summary.py $out/p*

@@ -92,16 +92,16 @@ def test_strict_matches_oracle_whole_frame(renderer, name):
     ref = oracle.render(scene, params, w, h, depth=depth, flags=cfg["flags"])
     _compare(gpu, ref, name)
     assert int((gpu["hits"][:, 0, 0] >= 0).sum()) > 0.5 * w * h or name == "c2"   # the frame is mostly scene
-    if name == "c5":   # the adaptive block order's second frame, and the per-bounce sorted wavefront
+    if name == "c5":   # the adaptive block order's second frame, and the unsorted queues
         _compare(renderer.render(w, h, depth=depth, flags=cfg["flags"] | STRICT, aux=True), ref, "c5 (2nd frame)")
-        _compare(renderer.render(w, h, depth=depth, flags=WAVEFRONT | WF_SORT | STRICT, aux=True), ref, "c5 sorted")
+        _compare(renderer.render(w, h, depth=depth, flags=WAVEFRONT | STRICT, aux=True), ref, "c5 unsorted")
 
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "c5"])
 def test_default_math_matches_reference_kernel(renderer, name, tmp_path):
     """S_ref (rt_render's default arithmetic) against the reference kernel as its host
     builds it, the whole frame at depth 3 with shadows (the reference's compiled-in
-    setting), on the config's scene and camera; C5 through its wavefront path, unsorted and sorted."""
+    setting), on the config's scene and camera; C5 through its wavefront path, sorted and unsorted."""
     scene, params, cfg = _config(name)
     w, h = cfg["w"], cfg["h"]
     ref = _reference(scene, params, w, h, tmp_path)
@@ -113,8 +113,8 @@ def test_default_math_matches_reference_kernel(renderer, name, tmp_path):
     print(f"{name}: S_ref depth 3 vs reference kernel: {nd} of {out.size} pixels differ")
     assert nd == 0
     assert int(np.sum(renderer.render(w, h, depth=3, flags=flags ^ WAVEFRONT if flags else WAVEFRONT) != ref)) == 0
-    if name == "c5":   # and the per-bounce sorted wavefront
-        assert int(np.sum(renderer.render(w, h, depth=3, flags=WAVEFRONT | WF_SORT) != ref)) == 0
+    if name == "c5":   # and the unsorted wavefront
+        assert int(np.sum(renderer.render(w, h, depth=3, flags=WAVEFRONT) != ref)) == 0
     if cfg["depth"] == 1:
         # the depth-1 frame's rays are bounce 0 of the pinned depth-3 frame
         d3 = renderer.render(w, h, depth=3, aux=True)
