@@ -836,6 +836,26 @@ def run(args, world, result_out=None):
                 "fetch_counts_cameras": len(fetch_cams)}
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         roof["peak_ns_per_record_per_cu"] = round(world * cus / peak_rps * 1e9, 3)
+        # The latency roof: a traversal iteration is a dependent fetch, so a wave's
+        # iterations form a chain.  rt_chase_peak times one dependent traversal-shaped iteration of a
+        # wave with every wave slot of the chip (8 per SIMD) running such a chain through an L2-resident
+        # table, the lanes of a quad on one chain; the frame's wave iterations spread over those slots
+        # then take at least iterations / slots * that time.
+        ch_iters = 512
+        lat = {}
+        for grp in (4, 1, 64):
+            ch_ms, ch_waves = r.chase_peak(16384, ch_iters, grp)
+            lat[grp] = (ch_ms / ch_iters, ch_waves)
+        t_iter_ms, slots = lat[4]
+        model_ms = ft["wave_instructions"] / (world * slots) * t_iter_ms
+        roof["latency"] = {
+            "roof": "wave iterations of the frame (counted on the GPU) / wave slots x the time of one dependent "
+                    "traversal-shaped iteration at full occupancy (rt_chase_peak, quad-coherent chains, L2-resident)",
+            "wave_iterations_per_frame": ft["wave_instructions"], "wave_slots": world * slots,
+            "ns_per_dependent_iteration": round(t_iter_ms * 1e6, 1),
+            "ns_per_dependent_iteration_lane_distinct": round(lat[1][0] * 1e6, 1),
+            "ns_per_dependent_iteration_wave_uniform": round(lat[64][0] * 1e6, 1),
+            "model_ms": round(model_ms, 4), "frac": round(model_ms / ms_per_step, 4)}
     if roof is None:   # the fused path, or --no-roofline: the HBM model of SURVEY 8d
         roof = {"bound": "hbm", "unit": "GB/s", "achieved": hbm["achieved_gbs"], "peak": HBM_PEAK_GBS,
                 "frac": round(hbm["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,

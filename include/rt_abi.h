@@ -300,6 +300,13 @@ int rt_timing_average(rt_ctx* ctx, int32_t n, float* total_ms, float* traverse_m
  * table_records 64-B records, iters (multiple of 4) per lane: ms per launch and records read. */
 int rt_fetch_counts(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint64_t* out8);
 int rt_gather_peak(rt_ctx* ctx, uint32_t table_records, uint32_t iters, float* ms, uint64_t* records);
+/* rt_chase_peak measures the other roof, latency: every wave of 8 per SIMD on every CU walks
+ * a chain of `iters` dependent traversal-shaped iterations (three 16-B + one 8-B load of a
+ * 64-B record, a dependent slab-like computation, the next record picked from the record's
+ * two references) through a table of table_records records, `group` lanes (1, 2, 4, ..., 64)
+ * following one chain: ms per launch and the number of waves (ms / iters = one dependent
+ * iteration of a wave with the chip full). */
+int rt_chase_peak(rt_ctx* ctx, uint32_t table_records, uint32_t iters, uint32_t group, float* ms, uint64_t* waves);
 
 /* Traversals of the last frame that outgrew the fast kernel's LDS stack and
  * restarted in-kernel with the general traversal (same result, slower ray);

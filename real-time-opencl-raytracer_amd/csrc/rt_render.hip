@@ -396,6 +396,35 @@ __global__ void __launch_bounds__(256) gather_peak_kernel(const float4* __restri
     if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;   // keeps the loads; practically never taken
 }
 
+// Dependent-fetch latency (rt_chase_peak, the latency roof of DESIGN.md 6.3): every wave of
+// 8 per SIMD on every CU walks `iters` steps of a chain through a table of inner-record-
+// shaped 64-B records, like one traversal iteration each: three 16-B loads + one 8-B load
+// of the current record, a slab-like dependent chain of packed ops on the boxes, and the
+// next record chosen by the result between the record's two child references.  The lanes
+// of a quad (group = 4) -- or `group` lanes -- follow one chain, as the lanes of a quad of
+// coherent rays do.  Time per launch / iters = the time of one dependent iteration of a
+// wave when every wave slot of the chip runs such a chain.
+__global__ void __launch_bounds__(256) chase_peak_kernel(const float4* __restrict__ table, uint32_t nrec, uint32_t iters,
+                                                         uint32_t group, uint32_t* __restrict__ sink) {
+    const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+    uint32_t idx = ((gid / group) * 2654435761u) % nrec;
+    float acc = 0.0f;
+    for (uint32_t i = 0; i < iters; ++i) {
+        const float4* p = table + (size_t)idx * 4;
+        const float4 q0 = p[0], q1 = p[1], q2 = p[2];
+        const float2 r = *reinterpret_cast<const float2*>(p + 3);
+        // both children's slab intervals from the loaded planes (dependent on the data)
+        const float n0 = fmaxf(fmaxf(q0.x * 0.5f - acc, q1.x * 0.5f), q2.x * 0.5f);
+        const float f0 = fminf(fminf(q0.z * 0.5f, q1.z * 0.5f - acc), q2.z * 0.5f);
+        const float n1 = fmaxf(fmaxf(q0.y * 0.5f, q1.y * 0.5f - acc), q2.y * 0.5f);
+        const float f1 = fminf(fminf(q0.w * 0.5f - acc, q1.w * 0.5f), q2.w * 0.5f);
+        const bool left = (f0 - n0) >= (f1 - n1);
+        idx = __float_as_uint(left ? r.x : r.y);
+        acc = (n0 + f1) * 1e-30f;
+    }
+    if (idx == 0xFFFFFFFFu) sink[blockIdx.x] = __float_as_uint(acc);   // keeps the chain; never taken
+}
+
 // Band re-interleave on rank 0 (rt_assemble_bands[_batch]): one block per frame row and
 // frame (grid h x nframes), 16-B copies when rows and slots are 16-B aligned.  Pure HBM
 // copy: 8 B/pixel.  Rank r's slot starts at r * slot_pixels and holds the frames' band
@@ -1627,6 +1656,63 @@ int rt_gather_peak(rt_ctx* c, uint32_t table_records, uint32_t iters, float* ms,
     if (e != hipSuccess) return set_err(c, std::string("rt_gather_peak: ") + hipGetErrorString(e), RT_ERR_DEVICE);
     *ms = t / 4.0f;
     *records = (uint64_t)blocks * 256u * iters;
+    return RT_OK;
+}
+
+int rt_chase_peak(rt_ctx* c, uint32_t table_records, uint32_t iters, uint32_t group, float* ms, uint64_t* waves) {
+    if (!c || !ms || !waves || table_records < 2 || iters == 0 || group == 0 || group > 64 || (64 % group))
+        return set_err(c, "rt_chase_peak: invalid argument", RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    int cus = 0;
+    HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    const uint32_t blocks = (uint32_t)cus * 8u;   // 8 blocks of 4 waves per CU: 8 waves per SIMD
+    // the table: random child references (two per record, both valid), boxes from a fixed pattern
+    std::vector<float4> tab((size_t)table_records * 4);
+    uint32_t x = 0x9E3779B9u;
+    for (uint32_t i = 0; i < table_records; ++i) {
+        uint32_t rr[2];
+        for (uint32_t& v : rr) {
+            x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+            v = x % table_records;
+        }
+        const float a = (float)(i % 97), b = (float)(i % 89);
+        tab[(size_t)i * 4 + 0] = make_float4(a, b, a + 3.0f, b + 5.0f);
+        tab[(size_t)i * 4 + 1] = make_float4(b, a, b + 7.0f, a + 2.0f);
+        tab[(size_t)i * 4 + 2] = make_float4(a + 1.0f, b + 1.0f, a + 9.0f, b + 4.0f);
+        float r0, r1;
+        std::memcpy(&r0, &rr[0], 4);
+        std::memcpy(&r1, &rr[1], 4);
+        tab[(size_t)i * 4 + 3] = make_float4(r0, r1, 0.0f, 0.0f);
+    }
+    float4* table = nullptr;
+    uint32_t* sink = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPC(c, hipMalloc((void**)&table, tab.size() * sizeof(float4)));
+    hipError_t e = hipMalloc((void**)&sink, blocks * 4);
+    if (e == hipSuccess) e = hipMemcpy(table, tab.data(), tab.size() * sizeof(float4), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(rtk::chase_peak_kernel, dim3(blocks), dim3(256), 0, c->stream, table, table_records, iters, group, sink);
+        e = hipEventRecord(e0, c->stream);
+    }
+    if (e == hipSuccess) {
+        for (int k = 0; k < 4; ++k)
+            hipLaunchKernelGGL(rtk::chase_peak_kernel, dim3(blocks), dim3(256), 0, c->stream, table, table_records, iters,
+                               group, sink);
+        e = hipEventRecord(e1, c->stream);
+    }
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float t = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(table);
+    if (sink) (void)hipFree(sink);
+    if (e != hipSuccess) return set_err(c, std::string("rt_chase_peak: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    *ms = t / 4.0f;
+    *waves = (uint64_t)blocks * 4u;
     return RT_OK;
 }
 

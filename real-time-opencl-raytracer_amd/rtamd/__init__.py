@@ -87,7 +87,7 @@ ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt
                "rt_peer_access", "rt_frame_sync_words", "rt_bands_put_sync", "rt_frame_present", "rt_frame_release",
                "rt_frame_sync_status", "rt_frame_checksum",
                "rt_scene_image_size", "rt_scene_image_pack",
-               "rt_scene_image_load", "rt_fetch_counts", "rt_gather_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_scene_image_load", "rt_fetch_counts", "rt_gather_peak", "rt_chase_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
@@ -147,6 +147,7 @@ def lib() -> C.CDLL:
             "rt_scene_image_load": (C.c_int, [vp, vp, C.c_uint64, vp]),
             "rt_fetch_counts": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(C.c_uint64)]),
             "rt_gather_peak": (C.c_int, [vp, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
+            "rt_chase_peak": (C.c_int, [vp, u32, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
             "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
             "rt_last_deferred": (C.c_int, [vp, C.POINTER(u32)]),
@@ -470,6 +471,12 @@ class Renderer:
         return {"inner": int(out[0]), "tri": int(out[1]), "quad_inner": int(out[2]), "quad_tri": int(out[3]),
                 "distinct_inner": int(out[4]), "distinct_tri": int(out[5]), "wave_instructions": int(out[6]),
                 "mixed_instructions": int(out[7])}
+
+    def chase_peak(self, table_records: int = 16384, iters: int = 512, group: int = 4):
+        """rt_chase_peak: (ms per launch, waves) of the dependent-iteration latency roof."""
+        ms, waves = C.c_float(), C.c_uint64()
+        _check(lib().rt_chase_peak(self._h, table_records, iters, group, C.byref(ms), C.byref(waves)), self._h)
+        return ms.value, waves.value
 
     def gather_peak(self, table_records: int = 16384, iters: int = 256):
         """rt_gather_peak: (ms per launch, records read) of the random-record gather ceiling."""

@@ -550,3 +550,14 @@ def test_refill_kernel_odd_sizes_and_bands(renderer):
         renderer.set_params(p)
         _compare(renderer.render(w, h, depth=1, flags=STRICT | REFILL, aux=True), _oracle(d, 1, w=w, h=h, params=p),
                  f"refill {w}x{h}")
+
+
+def test_latency_and_gather_roofs_measure(renderer):
+    """rt_chase_peak / rt_gather_peak return sane ceilings: a dependent iteration takes longer
+    than an independent record fetch, and coherent chains are no slower than distinct ones."""
+    ms4, waves = renderer.chase_peak(16384, 256, 4)
+    ms1, _ = renderer.chase_peak(16384, 256, 1)
+    ms64, _ = renderer.chase_peak(16384, 256, 64)
+    assert waves > 0 and 0 < ms64 <= ms4 * 1.05 and ms4 <= ms1 * 1.05
+    pk_ms, pk_n = renderer.gather_peak(16384, 256)
+    assert pk_ms > 0 and pk_n > 0
