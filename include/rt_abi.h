@@ -90,9 +90,6 @@ enum {
                                 waves; pixels are identical either way */
     RT_FLAG_EXACT_DIV = 4u,  /* force the division form of the slab test (volumeRender.cl:614-615) instead
                                 of the bit-identical fast quotient; for A/B only */
-    RT_FLAG_REFILL = 256u,   /* depth-1 frames: persistent waves whose quads of lanes take the frame's next
-                                2x2 pixels as soon as their own are done (first_bounce_refill_kernel),
-                                instead of one wave per 8x8 tile; pixels are identical either way */
     RT_FLAG_STATIC_ORDER = 16u /* keep the static XCD-dealt block order instead of the adaptive
                                 longest-first order built from the previous frame's per-block times
                                 (DESIGN.md 6.2); pixels are identical either way */

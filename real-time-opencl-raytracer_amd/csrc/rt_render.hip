@@ -666,7 +666,6 @@ struct rt_ctx {
     uint32_t order_tx = 0, order_ty = 0;
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
-    int refill_grid[3][2] = {{0, 0}, {0, 0}, {0, 0}};   // persistent depth-1 refill grid per math mode (, traced)
     struct { bool on = false; unsigned long long* d_counts = nullptr; } trace;   // rt_fetch_counts
     bool timing_valid = false;
     std::string err;
@@ -824,9 +823,6 @@ template <int M> struct Kernels;
             return next ? (void*)NS::first_bounce_kernel<true, true, true> : (void*)NS::first_bounce_kernel<true, false, true>; \
         }                                                                                                  \
         static void* traced_bounce() { return (void*)NS::wf_bounce_kernel<true, true>; }                  \
-        static void* refill(bool traced) {                                                                 \
-            return traced ? (void*)NS::first_bounce_refill_kernel<true> : (void*)NS::first_bounce_refill_kernel<false>; \
-        }                                                                                                  \
     };
 RTK_KERNELS(0, rtk_strict)
 RTK_KERNELS(1, rtk_hw)
@@ -844,9 +840,6 @@ static void* kernel_traced(int m, bool next) {
 }
 static void* kernel_traced_bounce(int m) {
     return m == 0 ? Kernels<0>::traced_bounce() : m == 1 ? Kernels<1>::traced_bounce() : Kernels<2>::traced_bounce();
-}
-static void* kernel_refill(int m, bool traced) {
-    return m == 0 ? Kernels<0>::refill(traced) : m == 1 ? Kernels<1>::refill(traced) : Kernels<2>::refill(traced);
 }
 static void* kernel_bounce(int m, bool fast) {
     return m == 0 ? Kernels<0>::bounce(fast) : m == 1 ? Kernels<1>::bounce(fast) : Kernels<2>::bounce(fast);
@@ -1435,35 +1428,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         if (depth > 1 && (rc = ensure(c, L.d_wq[0], L.wq_cap[0], qcap))) return rc;
         if (depth > 1 && (rc = ensure(c, L.d_wq[1], L.wq_cap[1], qcap))) return rc;
         const bool sort = (flags & RT_FLAG_WF_SORT) && depth > 1;
-        // depth 1 on a clean scene in one buffer: the quad-refill kernel (RT_FLAG_REFILL)
-        const bool refill = depth == 1 && fast && (flags & RT_FLAG_REFILL);
         // the local sort's key axis: the scene box's thinnest
         const float ext[3] = {F.smax.x - F.smin.x, F.smax.y - F.smin.y, F.smax.z - F.smin.z};
         const uint32_t thin = ext[1] <= ext[0] && ext[1] <= ext[2] ? 1u : ext[2] < ext[0] ? 2u : 0u;
         if (sort && (rc = ensure(c, L.d_perm, L.perm_cap, (size_t)npix))) return rc;
         auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)L.d_wq[k & 1] : (rtk::QRay*)nullptr; };
-        if (refill) {
-            // depth 1 with quad refill: persistent waves over the frame's quads (static tile order,
-            // no per-block times: the dynamic quad counter balances the waves)
-            int& g = c->refill_grid[math][traced ? 1 : 0];
-            if (!g) {
-                int cus = 0, b1 = 0;
-                HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-                HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (const void*)kernel_refill(math, traced), 256, 0));
-                g = std::max(8, std::max(b1, 1) * cus);
-                if (getenv("RTAMD_DEBUG")) fprintf(stderr, "refill grid: %d blocks (%d per CU x %d CUs)\n", g, b1, cus);
-            }
-            rtk::Frame Fr = F;
-            Fr.tile_order = c->d_order;
-            Fr.tile_cost = nullptr;
-            if (traced) O.fcount = c->trace.d_counts;
-            uint32_t* quad_counter = cnt + 2;   // bounce 0's fetch cursor, zeroed with the frame's counters
-            static const uint32_t batch = getenv("RTAMD_REFILL_BATCH") ? (uint32_t)atoi(getenv("RTAMD_REFILL_BATCH")) : 4u;
-            uint32_t bt = std::max(1u, std::min(16u, batch));
-            void* args[] = {&S, &Fr, &O, &ax, &quad_counter, &bt};
-            HIPC(c, hipLaunchKernel(kernel_refill(math, traced), dim3(g), block, args, 0, s));
-            ++L.nframe;
-        } else {
+        {
             rtk::WQ W{};
             W.out = depth > 1 ? qbuf(1) : nullptr;
             W.out_count = cnt + 8 * 1 + 0;

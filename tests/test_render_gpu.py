@@ -520,38 +520,6 @@ def test_records_beyond_the_buffer_load_limit_render_with_the_general_traversal(
     renderer.upload(_scene(d))   # back to one allocation for the tests that follow
 
 
-REFILL = 256   # RT_FLAG_REFILL
-
-
-@pytest.mark.parametrize("name", golden_names())
-@pytest.mark.parametrize("flags", [0, 1])
-def test_refill_kernel_matches_oracle(renderer, name, flags):
-    """Depth-1 frames on the quad-refill kernel (persistent waves, quads take the next
-    2x2 pixels when done): hits, t, rgb and pixels bit-exact vs the oracle, with and without
-    the shadow ray; and the same pixels as the tile kernel in the default arithmetic."""
-    d = load_golden(name)
-    renderer.upload(_scene(d))
-    renderer.set_params(d["params"])
-    w, h = int(d["w"]), int(d["h"])
-    gpu = renderer.render(w, h, depth=1, flags=flags | STRICT | REFILL, aux=True)
-    _compare(gpu, _oracle(d, 1, flags), f"{name} refill flags={flags}")
-    for f in (0, 2):
-        assert np.array_equal(renderer.render(w, h, depth=1, flags=flags | f | REFILL),
-                              renderer.render(w, h, depth=1, flags=flags | f))
-
-
-def test_refill_kernel_odd_sizes_and_bands(renderer):
-    import rtamd
-    d = load_golden("knot16k")
-    renderer.upload(_scene(d))
-    for (w, h) in [(1, 1), (17, 9), (123, 77), (1920, 8)]:
-        m = rtamd.Mesh.torus_knot(128, 64)
-        p = rtamd.params_to_array(m.camera_params(w, h))
-        renderer.set_params(p)
-        _compare(renderer.render(w, h, depth=1, flags=STRICT | REFILL, aux=True), _oracle(d, 1, w=w, h=h, params=p),
-                 f"refill {w}x{h}")
-
-
 def test_latency_and_gather_roofs_measure(renderer):
     """rt_chase_peak / rt_gather_peak return sane ceilings: a dependent iteration takes longer
     than an independent record fetch, and coherent chains are no slower than distinct ones."""
