@@ -48,7 +48,8 @@ def main():
         rows = sorted((r for r in csv.DictReader(open(trace[0])) if KERNEL in r["Kernel_Name"]),
                       key=lambda r: int(r["Start_Timestamp"]))
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
-        t = d[1 + j["warmup"]: 1 + j["warmup"] + j["steps"]]
+        wf = j.get("warmup_frames_run", j["warmup"])   # bench.py's time-based warm-up runs more frames
+        t = d[1 + wf: 1 + wf + j["steps"]]
         timed_us = round(sum(t) / len(t), 2) if t else None
         hip_ms = j["roofline"]["kernel_ms"]
     fetch, nf, ff = counter("prof_fetch", "FETCH_SIZE")
