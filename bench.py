@@ -310,6 +310,8 @@ def run(args, world, result_out=None):
         if world != 1:
             raise SystemExit("--shard is a single-process diagnostic")
         shard_r, shard_n = (int(v) for v in args.shard.split("/"))
+        if use_dist and shard_r != 0:
+            raise SystemExit("--dist --shard R/N: only R = 0 (rank 0's exchange work)")
     tiling = rtamd.rt_tiling(shard_r, shard_n, args.band_rows, 0)
     npx = rtamd.tiling_pixels(w, h, shard_r, shard_n, args.band_rows)
     cap = rtamd.tiling_pixels(w, h, 0, shard_n, args.band_rows)  # rank 0 owns the most bands
@@ -424,6 +426,10 @@ def run(args, world, result_out=None):
             sync_local = torch.zeros(NB, dtype=torch.int32, device=dev)   # this rank's per-set block counters
             fsync = rtamd.FrameSync(w, h, tiling, shard_n, NB, fr_base + 4 * nfr_words, sync_local.data_ptr(),
                                     args.sync_timeout_ms)
+            if args.shard:   # the N-1 shards no process puts: their arrivals never hold the present up
+                a0 = nfr_words + sync_words - NB * shard_n   # arrive[set][rank] ends the block
+                arrive = shared_all[a0:a0 + NB * shard_n].view(NB, shard_n)
+                arrive[:, 1:] = -1   # 0xFFFFFFFF >= every use
             use = [0] * NB   # times set j has been filled
     # frame checks: the camera index of every frame a set last held, and (--frame-check
     # every, rank 0) each presented frame's checksum, taken on its stream right after the

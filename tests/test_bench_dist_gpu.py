@@ -38,6 +38,20 @@ def test_bench_dist_path_assembles_the_frame(i, extra):
     assert res["value"] > 0 and res["n_gpus"] == 1
 
 
+@pytest.mark.parametrize("gather", ["ipc", "native"])
+def test_bench_dist_shard_diagnostic_completes(gather):
+    """--dist --shard 0/8: rank 0's exchange work at N = 8 with one process behind it (the
+    frame-sync block counts the processes that put, not the shards)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29631 + (gather == "native")))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist", "--shard", "0/8", "--gather", gather,
+           "--config", "c2", "--direct", "--steps", "8", "--warmup", "2", "--warmup-seconds", "0",
+           "--no-cpu-baseline", "--sync-timeout-ms", "2000", "--hang-timeout", "100"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["value"] > 0 and "shard 0/8" in res["config"]["parallelism"]
+
+
 def _ranks_on_one_gpu(n, extra, timeout=115):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
