@@ -94,15 +94,28 @@ struct Frame {
 struct QRay {
     float4 a, b, c;
 };
+// Ray queues are SEGMENTED: segment s holds slots [64 s, 64 s + 64) and the rays one wave
+// appended, packed from its first slot; seg_cnt[s] says how many.  The producer's wave of
+// segment s is a screen tile's 8x8 pixels (bounce 0) or the 64-ray group s of the previous
+// bounce's order, so the segments are in screen order and no append contends for a counter.
+// The producer also adds each count to its chunk's (16 segments) and super-chunk's (1024
+// segments) sum, from which wf_compact_sort_kernel's blocks find where their chunk starts
+// in the bounce's dense order `perm` (compacted, optionally sorted), with no scan launch.
+constexpr uint32_t kChunkSegs = 16, kSuperSegs = 1024;
 struct WQ {
-    const QRay* in;           // this bounce's rays
-    const uint32_t* in_count;
-    const uint32_t* perm;     // optional order of `in` (sorted), or null
+    const QRay* in;           // this bounce's rays (segmented)
+    const uint32_t* in_count; // rays in it
+    const uint32_t* perm;     // dense order of `in`: i -> slot
     QRay* out;                // next bounce's rays (null: none)
-    uint32_t* out_count;
-    uint32_t* fetch;          // dynamic work counter of this launch
+    uint32_t* seg_cnt;        // rays per segment of `out`
+    uint32_t* chunk_sum;      // rays per kChunkSegs segments of `out` (zeroed per frame)
+    uint32_t* super_sum;      // rays per kSuperSegs segments of `out` (zeroed per frame)
+    uint32_t seg;             // the segment this wave appends to (set per wave)
+    uint32_t* seg_fill;       // the wave's LDS word: rays appended to `seg` so far
+    uint32_t* fetch;          // the launch's work cursor
     int bounce;
 };
+constexpr uint32_t kSegRays = 64;
 
 struct Outputs {
     uint32_t* out;
@@ -215,17 +228,31 @@ __device__ __forceinline__ void zero_next_counters(const Frame& F) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < F.nzero; i += n) F.zero_next[i] = 0u;
 }
 
-// Wave-aggregated append: lanes with `want` get consecutive slots of `q`.
-// A queue slot for every active lane of the wave (one atomic per wave; lanes keep their
-// order, so the queue keeps the screen order of the waves that fill it).
-__device__ __forceinline__ QRay* wf_slot(QRay* q, uint32_t* count) {
+// Append to the wave's own segment: the active lanes get the next slots of segment `seg`,
+// in lane order.  The fill count is an LDS word of the wave, taken by the group's first
+// lane, so lanes that arrive in separate groups (if the wave has not reconverged) still
+// get distinct slots.
+__device__ __forceinline__ QRay* seg_slot(QRay* q, uint32_t seg, uint32_t* fill) {
     const uint64_t m = __builtin_amdgcn_ballot_w64(true);
     const int lane = threadIdx.x & 63;
     const int leader = __builtin_ctzll(m);
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__builtin_popcountll(m));
-    base = __shfl(base, leader);
-    return q + base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+    if (lane == leader) base = atomicAdd(fill, (uint32_t)__builtin_popcountll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    return q + (size_t)seg * kSegRays + base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+}
+// (all 64 lanes, after the wave's appends) the segment's count, also added to its chunk's
+// and super-chunk's sums; the fill word is reset for the wave's next segment
+__device__ __forceinline__ void seg_close(const WQ& W, uint32_t seg) {
+    if ((threadIdx.x & 63u) == 0) {
+        const uint32_t c = *W.seg_fill;
+        W.seg_cnt[seg] = c;
+        if (c) {
+            atomicAdd(W.chunk_sum + seg / kChunkSegs, c);
+            atomicAdd(W.super_sum + seg / kSuperSegs, c);
+        }
+        *W.seg_fill = 0u;
+    }
 }
 
 // Longest-first block order (LPT list scheduling): the hardware hands blocks to free CU
@@ -294,43 +321,67 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
 
 // ---- math-independent kernels ----
 
-// Per-bounce local sort (RT_FLAG_WF_SORT): block b reorders queue entries [1024b, 1024b+1024)
-// -- rays from one screen-local region, since the queue keeps the screen order of the waves
-// that appended them -- by the component of their direction along the scene box's thinnest
-// axis (8 buckets of width 1/4, counting sort in LDS), into perm.  Rays that leave the scene's slab
-// steeply take few steps, rays running along it many: grouping them by that component puts
-// rays of similar length (and similar direction) into the same waves of 64, where a wave runs
-// as long as its longest ray.  Simulated on C5's bounce queues (the oracle's per-ray step
-// counts): wave iterations -26 % at bounce 1, -24 % at bounce 2 against the queue order with
-// 32 buckets; measured, finer buckets cost more in lost fetch sharing between neighbouring
-// rays than they save (C5 ms per frame, 1000 frames: unsorted 1.000-1.002; 2 buckets 1.023,
-// 4 0.970-0.972, 6 0.965, 8 0.968-0.970, 12 0.978, 16 0.983, 32 1.004-1.005;
-// profiles/r03/c5_sort/).
-constexpr uint32_t kLocalSortChunk = 1024;
-// Stable: inside a bucket the rays keep their queue order, so neighbouring pixels (a quad's
+// Dense order of a segmented queue (wf_compact_sort_kernel): block b takes the 16 segments
+// [16 b, 16 b + 16), i.e. 1024 slots of one screen-local region (4 tiles of 16x16 pixels at
+// bounce 1), finds where its rays start in the dense order from the super-chunk and chunk
+// sums before it (d0), and writes perm[d0 ..] with their slots, in slot order -- or with
+// `sort` (RT_FLAG_WF_SORT), stably by the
+// component of the ray's direction along the scene box's thinnest axis (8 buckets of width
+// 1/4).  Rays that leave the scene's slab steeply take few steps, rays running along it
+// many: grouping them by that component puts rays of similar length (and similar direction)
+// into the same waves of 64, where a wave runs as long as its longest ray.  Simulated on
+// C5's bounce queues (the oracle's per-ray step counts): wave iterations -26 % at bounce 1,
+// -24 % at bounce 2 against the queue order with 32 buckets; measured, finer buckets cost
+// more in lost fetch sharing between neighbouring rays than they save (C5 ms per frame,
+// round 3 before the segmented queues: unsorted 1.000-1.002; 2 buckets 1.023, 4 0.970-0.972,
+// 6 0.965, 8 0.968-0.970, 12 0.978, 16 0.983, 32 1.004-1.005; profiles/r03/c5_sort/).
+// Stable: inside a bucket the rays keep their slot order, so neighbouring pixels (a quad's
 // four rays, appended side by side) stay side by side and keep sharing their record fetches.
-// Entry i = c0 + 256 p + t is ranked among the entries of its bucket by (pass p, wave, lane):
+// Slot j = c0 + 256 p + t is ranked among the entries of its bucket by (pass p, wave, lane):
 // peers in a wave by a 3-bit ballot match, earlier waves and passes by LDS counts.
-__global__ void __launch_bounds__(256) wf_local_sort_kernel(const QRay* __restrict__ q, const uint32_t* __restrict__ count,
-                                                            uint32_t* __restrict__ perm, uint32_t axis) {
+// The block of the queue's last segment stores the queue's size in *total.  nseg is
+// `nseg_fixed` (bounce 1: the first bounce's waves), or when 0 the previous bounce's 64-ray
+// groups, ceil(*prev_total / 64).
+constexpr uint32_t kLocalSortChunk = kChunkSegs * kSegRays;
+__global__ void __launch_bounds__(256) wf_compact_sort_kernel(const QRay* __restrict__ q,
+                                                              const uint32_t* __restrict__ seg_cnt,
+                                                              const uint32_t* __restrict__ chunk_sum,
+                                                              const uint32_t* __restrict__ super_sum, uint32_t nseg_fixed,
+                                                              const uint32_t* __restrict__ prev_total,
+                                                              uint32_t* __restrict__ total_out, uint32_t* __restrict__ perm,
+                                                              uint32_t axis, uint32_t sort) {
     constexpr uint32_t kPasses = kLocalSortChunk / 256;
     constexpr uint32_t kBuckets = 8;
     __shared__ uint32_t cnt[kBuckets][kPasses * 4];   // [bucket][pass * 4 + wave]: entries, then their offsets
     __shared__ uint32_t total[kBuckets];
-    const uint32_t n = *count, t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    const uint32_t c0 = blockIdx.x * kLocalSortChunk;
-    if (c0 >= n) return;   // the grid covers the queue's capacity
+    __shared__ uint32_t segc[kChunkSegs];
+    __shared__ uint32_t part[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint32_t nseg = nseg_fixed ? nseg_fixed : (*prev_total + kSegRays - 1) / kSegRays;
+    const uint32_t b = blockIdx.x, s0 = b * kChunkSegs;
+    if (s0 >= nseg) return;   // the grid covers the queue's capacity
+    const uint32_t c0 = s0 * kSegRays;
+    // d0 = rays in the super-chunks, then the chunks of this super-chunk, before this chunk
+    constexpr uint32_t kChunksPerSuper = kSuperSegs / kChunkSegs;
+    const uint32_t nsup = b / kChunksPerSuper, nch = b % kChunksPerSuper;
+    uint32_t x = 0;
+    for (uint32_t i = t; i < nsup; i += 256) x += super_sum[i];
+    if (t < nch) x += chunk_sum[nsup * kChunksPerSuper + t];
+    for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_down((int)x, o);
+    if (lane == 0) part[wave] = x;
+    if (t < kChunkSegs) segc[t] = s0 + t < nseg ? seg_cnt[s0 + t] : 0u;
     for (uint32_t i = t; i < kBuckets * kPasses * 4; i += 256) (&cnt[0][0])[i] = 0u;
     __syncthreads();
+    const uint32_t d0 = part[0] + part[1] + part[2] + part[3];
     uint32_t key[kPasses], rank[kPasses];
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (uint32_t p = 0; p < kPasses; ++p) {
-        const uint32_t i = c0 + 256u * p + t;
-        const bool valid = i < n;
+        const uint32_t j = c0 + 256u * p + t;   // one segment per wave and pass
+        const bool valid = (j % kSegRays) < segc[(j - c0) / kSegRays];
         uint32_t k = 0;
-        if (valid) {
-            const float4 b = q[i].b;   // {d.xyz, shadow sum}
+        if (valid && sort) {
+            const float4 b = q[j].b;   // {d.xyz, shadow sum}
             const float d = axis == 0 ? b.x : axis == 1 ? b.y : b.z;
             k = d == d ? (uint32_t)min(max((int)((d + 1.0f) * 4.0f), 0), 7) : 0u;
         }
@@ -357,16 +408,17 @@ __global__ void __launch_bounds__(256) wf_local_sort_kernel(const QRay* __restri
     __syncthreads();
     if (t == 0) {   // bucket starts (exclusive prefix over buckets), kept in total[]
         uint32_t acc = 0;
-        for (uint32_t b = 0; b < kBuckets; ++b) {
-            const uint32_t c = total[b];
-            total[b] = acc;
+        for (uint32_t k = 0; k < kBuckets; ++k) {
+            const uint32_t c = total[k];
+            total[k] = acc;
             acc += c;
         }
+        if (s0 + kChunkSegs >= nseg) *total_out = d0 + acc;   // the queue's last chunk
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t p = 0; p < kPasses; ++p)
-        if (key[p] < kBuckets) perm[c0 + total[key[p]] + cnt[key[p]][p * 4 + wave] + rank[p]] = c0 + 256u * p + t;
+        if (key[p] < kBuckets) perm[d0 + total[key[p]] + cnt[key[p]][p * 4 + wave] + rank[p]] = c0 + 256u * p + t;
 }
 
 // Random-record gather ceiling (rt_gather_peak): every lane of every wave
@@ -652,7 +704,9 @@ struct rt_ctx {
         uint32_t* d_gstack = nullptr; size_t gstack_cap = 0;                // in pixels
         float4* d_wq[2] = {nullptr, nullptr}; size_t wq_cap[2] = {0, 0};   // wavefront ray queues (ping-pong)
         uint32_t* d_wcnt = nullptr; size_t wcnt_cap = 0;                    // frame counters, 2 parity sets
-        uint32_t* d_perm = nullptr; size_t perm_cap = 0;                    // wavefront sort: permutation
+        size_t wcnt_set = 0;                                                //   of this many words each
+        uint32_t* d_perm = nullptr; size_t perm_cap = 0;                    // wavefront: dense queue order
+        uint32_t* d_seg = nullptr; size_t seg_cap = 0;                      // wavefront: rays per queue segment
         uint32_t* d_cost = nullptr; size_t cost_cap = 0;   // adaptive order: per-tile times,
         uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;     //   the longest-first order built from them,
         uint32_t* d_done = nullptr;                        //   and the finished-block counter
@@ -673,9 +727,10 @@ struct rt_ctx {
 
 static std::string g_err;
 
-// frame counters (one parity set): 8 per bounce, then the restart count, then per bounce
-// the counting sort's bucket histogram and cursors (256 + 256)
-constexpr size_t kRestartSlot = 8 * (RT_MAX_DEPTH + 1);
+// frame counters (one parity set): 8 per bounce ([0] queue size, [2] the bounce launch's
+// work cursor), then the restart count (then, sized per frame, the queues' chunk sums)
+constexpr size_t kBounceWords = 8;
+constexpr size_t kRestartSlot = kBounceWords * (RT_MAX_DEPTH + 1);
 constexpr size_t kCounters = kRestartSlot + 1;
 
 static int set_err(rt_ctx* c, const std::string& m, int code) {
@@ -702,7 +757,7 @@ static int ensure(rt_ctx* c, T*& p, size_t& cap, size_t n) {
 
 static void free_slot(rt_ctx::FrameSlot& f) {
     for (void* p : {(void*)f.d_gstack, (void*)f.d_wq[0], (void*)f.d_wq[1], (void*)f.d_wcnt,
-                    (void*)f.d_perm, (void*)f.d_cost, (void*)f.d_lpt, (void*)f.d_done})
+                    (void*)f.d_perm, (void*)f.d_seg, (void*)f.d_cost, (void*)f.d_lpt, (void*)f.d_done})
         if (p) (void)hipFree(p);
     if (f.idle) (void)hipEventDestroy(f.idle);
     f = rt_ctx::FrameSlot{};
@@ -1351,16 +1406,23 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
 
     if ((rc = ensure(c, L.d_gstack, L.gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
     O.gstack = L.d_gstack;
-    // frame counters, two parity sets: [8k + 0] queue size of bounce k, [8k + 2] its fetch
-    // cursor, [kRestartSlot] restarted traversals, then the sort histograms
-    if (!L.d_wcnt) {
-        if ((rc = ensure(c, L.d_wcnt, L.wcnt_cap, 2 * kCounters))) return rc;
-        HIPC(c, hipMemsetAsync(L.d_wcnt, 0, 2 * kCounters * sizeof(uint32_t), s));
+    // frame counters, two parity sets: per bounce k (kBounceWords from kBounceWords k) its
+    // queue size and its work cursor; [kRestartSlot] restarted traversals; then per queue
+    // k = 1 .. its chunk sums and super-chunk sums (segmented queues, rtk::WQ)
+    const size_t nseg = (size_t)F.num_blocks * 4;   // bounce 0's waves; later queues have fewer groups
+    const size_t nchunk = (nseg + rtk::kChunkSegs - 1) / rtk::kChunkSegs;
+    const size_t nsuper = (nseg + rtk::kSuperSegs - 1) / rtk::kSuperSegs;
+    const size_t set_words = kCounters + (size_t)RT_MAX_DEPTH * (nchunk + nsuper);
+    if (!L.d_wcnt || L.wcnt_set < set_words) {
+        if ((rc = ensure(c, L.d_wcnt, L.wcnt_cap, 2 * set_words))) return rc;
+        HIPC(c, hipMemsetAsync(L.d_wcnt, 0, 2 * set_words * sizeof(uint32_t), s));
+        L.wcnt_set = set_words;
     }
     const uint64_t par = L.nframe & 1u;
-    uint32_t* cnt = L.d_wcnt + par * kCounters;
-    F.zero_next = L.d_wcnt + (par ^ 1u) * kCounters;
-    F.nzero = (uint32_t)kCounters;
+    uint32_t* cnt = L.d_wcnt + par * L.wcnt_set;
+    F.zero_next = L.d_wcnt + (par ^ 1u) * L.wcnt_set;
+    F.nzero = (uint32_t)L.wcnt_set;
+    auto sums = [&](int k) { return cnt + kCounters + (size_t)(k - 1) * (nchunk + nsuper); };   // queue k >= 1
     O.restarts = cnt + kRestartSlot;
 
     // static block order: a host-built table, rebuilt when the block grid changes
@@ -1424,19 +1486,26 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (const void*)kernel_bounce(math, true), 256, 0));
             c->wf_grid[math] = std::max(8, std::max(b1, 1) * cus);
         }
-        const size_t qcap = (size_t)npix * 3;  // float4 per QRay x 3
-        if (depth > 1 && (rc = ensure(c, L.d_wq[0], L.wq_cap[0], qcap))) return rc;
-        if (depth > 1 && (rc = ensure(c, L.d_wq[1], L.wq_cap[1], qcap))) return rc;
+        // segmented queues: bounce 0's waves (4 per block) each own a segment of 64 slots;
+        // later bounces have at most as many 64-ray groups
+        const size_t slots = nseg * rtk::kSegRays;
+        if (depth > 1) {
+            if ((rc = ensure(c, L.d_wq[0], L.wq_cap[0], slots * 3))) return rc;   // 3 float4 per QRay
+            if ((rc = ensure(c, L.d_wq[1], L.wq_cap[1], slots * 3))) return rc;
+            if ((rc = ensure(c, L.d_perm, L.perm_cap, slots))) return rc;
+            if ((rc = ensure(c, L.d_seg, L.seg_cap, nseg))) return rc;
+        }
         const bool sort = (flags & RT_FLAG_WF_SORT) && depth > 1;
         // the local sort's key axis: the scene box's thinnest
         const float ext[3] = {F.smax.x - F.smin.x, F.smax.y - F.smin.y, F.smax.z - F.smin.z};
         const uint32_t thin = ext[1] <= ext[0] && ext[1] <= ext[2] ? 1u : ext[2] < ext[0] ? 2u : 0u;
-        if (sort && (rc = ensure(c, L.d_perm, L.perm_cap, (size_t)npix))) return rc;
         auto qbuf = [&](int k) { return depth > 1 ? (rtk::QRay*)L.d_wq[k & 1] : (rtk::QRay*)nullptr; };
         {
             rtk::WQ W{};
             W.out = depth > 1 ? qbuf(1) : nullptr;
-            W.out_count = cnt + 8 * 1 + 0;
+            W.seg_cnt = L.d_seg;
+            W.chunk_sum = sums(1);
+            W.super_sum = sums(1) + nchunk;
             W.bounce = 0;
             void* args[] = {&S, &F, &O, &W, &ax};
             if (traced) {   // rt_fetch_counts: the counting instantiation of the same kernel
@@ -1458,17 +1527,19 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         for (int k = 1; k < depth; ++k) {  // bounce k over its queue
             rtk::WQ W{};
             W.in = qbuf(k);
-            W.in_count = cnt + 8 * k + 0;
-            W.perm = nullptr;
-            if (sort) {   // per-bounce local sort of the queue (wf_local_sort_kernel)
-                hipLaunchKernelGGL(rtk::wf_local_sort_kernel, dim3((uint32_t)((npix + rtk::kLocalSortChunk - 1) / rtk::kLocalSortChunk)),
-                                   dim3(256), 0, s, (const rtk::QRay*)qbuf(k), (const uint32_t*)(cnt + 8 * k + 0), L.d_perm,
-                                   thin);
-                W.perm = L.d_perm;
-            }
+            uint32_t* bc = cnt + kBounceWords * k;
+            W.in_count = bc;
+            // the queue's dense (compacted, optionally sorted) order and its size
+            hipLaunchKernelGGL(rtk::wf_compact_sort_kernel, dim3((uint32_t)nchunk), dim3(256), 0, s,
+                               (const rtk::QRay*)qbuf(k), (const uint32_t*)L.d_seg, (const uint32_t*)sums(k),
+                               (const uint32_t*)(sums(k) + nchunk), k == 1 ? (uint32_t)nseg : 0u,
+                               (const uint32_t*)(bc - kBounceWords), bc, L.d_perm, thin, sort ? 1u : 0u);
+            W.perm = L.d_perm;
             W.out = k + 1 < depth ? qbuf(k + 1) : nullptr;
-            W.out_count = cnt + 8 * (k + 1) + 0;
-            W.fetch = cnt + 8 * k + 2;
+            W.seg_cnt = L.d_seg;
+            W.chunk_sum = sums(k + 1);
+            W.super_sum = sums(k + 1) + nchunk;
+            W.fetch = bc + 2;
             W.bounce = k;
             void* args[] = {&S, &Fb, &O, &W, &ax};
             HIPC(c, hipLaunchKernel(traced ? kernel_traced_bounce(math) : kernel_bounce(math, fast), dim3(c->wf_grid[math]),
@@ -1556,7 +1627,7 @@ int rt_last_deferred(rt_ctx* c, uint32_t* count) {
     if (!L || !L->d_wcnt || L->nframe == 0) return RT_OK;
     HIPC(c, hipEventSynchronize(L->idle));
     const uint64_t par = (L->nframe - 1) & 1u;   // the last frame's parity set
-    HIPC(c, hipMemcpy(count, L->d_wcnt + par * kCounters + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPC(c, hipMemcpy(count, L->d_wcnt + par * L->wcnt_set + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
