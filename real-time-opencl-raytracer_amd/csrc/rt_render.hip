@@ -1412,7 +1412,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const size_t nseg = (size_t)F.num_blocks * 4;   // bounce 0's waves; later queues have fewer groups
     const size_t nchunk = (nseg + rtk::kChunkSegs - 1) / rtk::kChunkSegs;
     const size_t nsuper = (nseg + rtk::kSuperSegs - 1) / rtk::kSuperSegs;
-    const size_t set_words = kCounters + (size_t)RT_MAX_DEPTH * (nchunk + nsuper);
+    const size_t set_words = kCounters + (depth > 1 ? (size_t)(depth - 1) * (nchunk + nsuper) : 0);
     if (!L.d_wcnt || L.wcnt_set < set_words) {
         if ((rc = ensure(c, L.d_wcnt, L.wcnt_cap, 2 * set_words))) return rc;
         HIPC(c, hipMemsetAsync(L.d_wcnt, 0, 2 * set_words * sizeof(uint32_t), s));
@@ -1421,7 +1421,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const uint64_t par = L.nframe & 1u;
     uint32_t* cnt = L.d_wcnt + par * L.wcnt_set;
     F.zero_next = L.d_wcnt + (par ^ 1u) * L.wcnt_set;
-    F.nzero = (uint32_t)L.wcnt_set;
+    F.nzero = (uint32_t)L.wcnt_set;   // all of it: the next frame may be deeper than this one
     auto sums = [&](int k) { return cnt + kCounters + (size_t)(k - 1) * (nchunk + nsuper); };   // queue k >= 1
     O.restarts = cnt + kRestartSlot;
 

@@ -369,6 +369,29 @@ def test_wavefront_path_matches_oracle(renderer, name, depth, sort):
     _compare(renderer.render(w, h, depth=depth, flags=flags, aux=True), ref, f"{name} depth={depth} sort={sort} (2)")
 
 
+def test_wavefront_frames_of_changing_depth_and_size(renderer):
+    """One renderer (one stream, one frame slot) renders wavefront frames whose depth and
+    size change from frame to frame: the segmented queues, their chunk sums and the frame
+    counters (two parity sets, the next frame's zeroed by this one) are resized and reused;
+    every frame equals the oracle's."""
+    import rtamd
+    d = load_golden("knot16k")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    refs = {}
+    seq = [(3, w, h), (1, w, h), (3, w, h), (2, w // 2, h // 2), (3, w, h), (8, w // 2 + 5, h // 2 + 3),
+           (1, w // 2, h // 2), (3, w, h)]
+    for i, (depth, fw, fh) in enumerate(seq):
+        for sort in (False, True):
+            flags = STRICT | WAVEFRONT | (WF_SORT if sort else 0)
+            key = (depth, fw, fh)
+            if key not in refs:
+                refs[key] = _oracle(d, depth, w=fw, h=fh)
+            _compare(renderer.render(fw, fh, depth=depth, flags=flags, aux=True), refs[key],
+                     f"frame {i}: depth {depth} {fw}x{fh} sort={sort}")
+
+
 @pytest.mark.parametrize("name", golden_names())
 @pytest.mark.parametrize("depth", [1, 3])
 @pytest.mark.parametrize("sort", [False, True])
