@@ -373,14 +373,18 @@ def run(args, world, result_out=None):
     gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)] \
         if (use_dist and rank == 0 and not ipc) else None
     glists = [list(g.unbind(0))[:world] for g in gbufs] if gbufs is not None else [None] * NB
-    # rank 0's frames; on the ipc path followed, in the same allocation, by the frame-sync
-    # block (rt_frame_sync_words) that the ranks' puts and rank 0's presents share
+    # rank 0's frames.  On the ipc path they are followed, in the same allocation, by the
+    # frame-sync block (rt_frame_sync_words) that the ranks' puts and rank 0's presents share,
+    # and that allocation is uncached device memory (rt_shared_alloc): peers write it over
+    # xGMI while rank 0's kernels poll and read it.  Other paths: a torch tensor.
     nfr_words = NB * B * h * w
     sync_words = rtamd.frame_sync_words(NB, shard_n) if ipc else 0
-    shared_all = (torch.zeros(nfr_words + (sync_words + 3) // 4 * 4, dtype=torch.int32, device=dev)
-                  if (rank == 0 and use_dist) else None)
-    frames_all = shared_all[:nfr_words].view(NB, B, h * w) if shared_all is not None else None
-    frames = list(frames_all) if frames_all is not None else None
+    shm = None
+
+    def torch_frames():
+        t = torch.zeros(nfr_words, dtype=torch.int32, device=dev)
+        return list(t.view(NB, B, h * w))
+    frames = torch_frames() if (rank == 0 and use_dist and not ipc) else None
     shared = None
     fsync = None
     if ipc:
@@ -393,12 +397,13 @@ def run(args, world, result_out=None):
         try:
             if rank == 0:
                 try:
-                    hnd, off = rtamd.SharedFrames.export(local, shared_all.data_ptr())
+                    shm = rtamd.SharedAlloc(local, 4 * (nfr_words + sync_words))
+                    hnd, off = rtamd.SharedFrames.export(local, shm.ptr)
                     store.set("rtamd_ipc", hnd + off.to_bytes(8, "little") + local.to_bytes(4, "little"))
                 except rtamd.RtError:
                     store.set("rtamd_ipc", b"")
                     raise
-                fr_base = shared_all.data_ptr()
+                fr_base = shm.ptr
             else:
                 blob = bytes(store.get("rtamd_ipc"))
                 if len(blob) != rtamd.SharedFrames.HANDLE_BYTES + 12:
@@ -419,6 +424,10 @@ def run(args, world, result_out=None):
                 shared.close()
                 shared = None
             if rank == 0:
+                if shm is not None:
+                    shm.close()
+                    shm = None
+                frames = torch_frames()
                 gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)]
                 glists = [list(g.unbind(0))[:world] for g in gbufs]
         else:
@@ -428,8 +437,10 @@ def run(args, world, result_out=None):
                                     args.sync_timeout_ms)
             if args.shard:   # the N-1 shards no process puts: their arrivals never hold the present up
                 a0 = nfr_words + sync_words - NB * shard_n   # arrive[set][rank] ends the block
-                arrive = shared_all[a0:a0 + NB * shard_n].view(NB, shard_n)
-                arrive[:, 1:] = -1   # 0xFFFFFFFF >= every use
+                arrive = torch.full((NB, shard_n), -1, dtype=torch.int32, device=dev)   # 0xFFFFFFFF >= every use
+                arrive[:, 0] = 0
+                rtamd.copy_device(fr_base + 4 * a0, arrive.data_ptr(), arrive.numel() * 4, streams[0].cuda_stream)
+                torch.cuda.synchronize(dev)
             use = [0] * NB   # times set j has been filled
     # frame checks: the camera index of every frame a set last held, and (--frame-check
     # every, rank 0) each presented frame's checksum, taken on its stream right after the
@@ -658,9 +669,15 @@ def run(args, world, result_out=None):
 
         held = [(j, s) for j in range(NB) for s in range(filled[j]) if frame_of[j][s] >= 0]
         frame_ok = bool(held)
+        got_frame = torch.zeros(h * w, dtype=torch.int32, device=dev)
         for j, s in held:
             reference(frame_of[j][s] % L)
-            frame_ok = frame_ok and bool(torch.equal(full, frames[j][s]))
+            if ipc:   # the uncached shared frame, copied out
+                rtamd.copy_device(got_frame.data_ptr(), put_dst[j][s], 4 * h * w, streams[0].cuda_stream)
+                torch.cuda.synchronize(dev)
+            else:
+                got_frame = frames[j][s]
+            frame_ok = frame_ok and bool(torch.equal(full, got_frame))
         frame_check = {"held_frames_checked": len(held), "held_frames_equal": frame_ok,
                        "distinct_cameras": min(L, total_frames)}
         if check_every and sums is not None:

@@ -236,6 +236,14 @@ int rt_ipc_open(int32_t device, const uint8_t* handle, int32_t handle_bytes, voi
 int rt_ipc_close(int32_t device, void* d_base);
 int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
                  void* stream);
+/* Rank 0's shared frames + sync block for the IPC exchange: other GPUs write them over xGMI
+ * while rank 0's kernels poll and read them, so they must be coherent across devices during
+ * kernels -- uncached device memory (hipExtMallocWithFlags(hipDeviceMallocUncached)), zeroed,
+ * exportable with rt_ipc_export.  (Coarse-grained hipMalloc memory is coherent only at kernel
+ * boundaries.)  rt_copy_device: a device-to-device copy on `stream` (frame checks). */
+int rt_shared_alloc(int32_t device, uint64_t bytes, void** d_ptr);
+int rt_shared_free(int32_t device, void* d_ptr);
+int rt_copy_device(void* d_dst, const void* d_src, uint64_t bytes, void* stream);
 /* Whether `device` can map `peer`'s memory (hipDeviceCanAccessPeer; 1 for device == peer).
  * bench.py maps rank 0's frames only when every rank can; otherwise it uses the RCCL gather. */
 int rt_peer_access(int32_t device, int32_t peer, int32_t* can);

@@ -219,6 +219,40 @@ int rt_peer_access(int32_t device, int32_t peer, int32_t* can) {
     return RT_OK;
 }
 
+// Rank 0's shared frames + frame-sync block: written by other GPUs over xGMI while rank 0's
+// kernels poll and read them, so not coarse-grained hipMalloc memory (coherent only at kernel
+// boundaries) but uncached device memory (MTYPE UC: no L2 line can go stale on any GPU, the
+// same kind RCCL uses for its cross-GPU flags and FIFOs).  Zeroed.
+int rt_shared_alloc(int32_t device, uint64_t bytes, void** d_ptr) {
+    if (!d_ptr || bytes == 0) return comm_err("rt_shared_alloc: invalid argument", RT_ERR_INVALID_ARG);
+    *d_ptr = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return comm_err("rt_shared_alloc: hipSetDevice", RT_ERR_DEVICE);
+    hipError_t e = hipExtMallocWithFlags(d_ptr, (size_t)bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) {
+        *d_ptr = nullptr;
+        return comm_err(std::string("rt_shared_alloc: hipExtMallocWithFlags: ") + hipGetErrorString(e),
+                        RT_ERR_OUT_OF_MEMORY);
+    }
+    if ((e = hipMemset(*d_ptr, 0, (size_t)bytes)) != hipSuccess) {
+        (void)hipFree(*d_ptr);
+        *d_ptr = nullptr;
+        return comm_err(std::string("rt_shared_alloc: hipMemset: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    }
+    return RT_OK;
+}
+
+int rt_shared_free(int32_t device, void* d_ptr) {
+    if (!d_ptr) return RT_OK;
+    (void)hipSetDevice(device);
+    return hipFree(d_ptr) == hipSuccess ? RT_OK : comm_err("rt_shared_free: hipFree", RT_ERR_DEVICE);
+}
+
+int rt_copy_device(void* d_dst, const void* d_src, uint64_t bytes, void* stream) {
+    if ((!d_dst || !d_src) && bytes) return comm_err("rt_copy_device: invalid argument", RT_ERR_INVALID_ARG);
+    const hipError_t e = hipMemcpyAsync(d_dst, d_src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    return e == hipSuccess ? RT_OK : comm_err(std::string("rt_copy_device: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+}
+
 int rt_ipc_close(int32_t device, void* d_ptr) {
     if (!d_ptr) return RT_ERR_INVALID_ARG;
     (void)hipSetDevice(device);

@@ -85,7 +85,7 @@ ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt
                "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
                "rt_frame_ready_wait", "rt_ipc_export", "rt_ipc_open", "rt_ipc_close", "rt_bands_put",
                "rt_peer_access", "rt_frame_sync_words", "rt_bands_put_sync", "rt_frame_present", "rt_frame_release",
-               "rt_frame_sync_status", "rt_frame_checksum",
+               "rt_frame_sync_status", "rt_frame_checksum", "rt_shared_alloc", "rt_shared_free", "rt_copy_device",
                "rt_scene_image_size", "rt_scene_image_pack",
                "rt_scene_image_load", "rt_fetch_counts", "rt_gather_peak", "rt_chase_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
@@ -141,6 +141,9 @@ def lib() -> C.CDLL:
             "rt_frame_release": (C.c_int, [vp, i32, i32, u32, vp]),
             "rt_frame_sync_status": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32)]),
             "rt_frame_checksum": (C.c_int, [vp, C.c_uint64, vp, vp]),
+            "rt_shared_alloc": (C.c_int, [i32, C.c_uint64, C.POINTER(vp)]),
+            "rt_shared_free": (C.c_int, [i32, vp]),
+            "rt_copy_device": (C.c_int, [vp, vp, C.c_uint64, vp]),
             "rt_frame_ready_wait": (C.c_int, [vp, i32, vp]),
             "rt_scene_image_size": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
             "rt_scene_image_pack": (C.c_int, [vp, vp, C.c_uint64, vp]),
@@ -692,6 +695,34 @@ def bands_putter(w: int, h: int, tiling: Optional[rt_tiling] = None):
         if rc:
             _check(rc)
     return put
+
+
+class SharedAlloc:
+    """rt_shared_alloc: zeroed uncached device memory on `device` for rank 0's shared frames
+    and sync block (peers write it over xGMI while rank 0's kernels poll and read it).
+    .ptr; close() frees it."""
+
+    def __init__(self, device: int, nbytes: int):
+        p = C.c_void_p()
+        rc = lib().rt_shared_alloc(device, nbytes, C.byref(p))
+        if rc:
+            raise RtError(rc, lib().rt_comm_last_error().decode())
+        self.device, self.ptr, self.nbytes = device, p.value, nbytes
+
+    def close(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.rt_shared_free(self.device, self.ptr)
+            self.ptr = None
+
+    __del__ = close
+
+
+def copy_device(d_dst: int, d_src: int, nbytes: int, stream: int) -> None:
+    """rt_copy_device: device-to-device copy on `stream`."""
+    _stream_arg(stream)
+    rc = lib().rt_copy_device(d_dst, d_src, nbytes, stream)
+    if rc:
+        raise RtError(rc, lib().rt_comm_last_error().decode())
 
 
 def peer_access(device: int, peer: int) -> bool:

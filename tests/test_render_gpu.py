@@ -168,6 +168,51 @@ def test_band_puts_place_every_rank_into_the_frame(renderer, nranks, band_rows, 
     assert np.array_equal(frame.cpu().numpy().view(np.uint32), full)
 
 
+def test_uncached_shared_frames_take_puts_and_sync(renderer):
+    """rt_shared_alloc (rank 0's shared frames + sync block for the IPC exchange, uncached so
+    peers' xGMI writes and rank 0's in-kernel polling are coherent across GPUs): zeroed, IPC
+    exportable, and a 3-rank frame put into it with rt_bands_put_sync and presented with
+    rt_frame_present equals a one-rank render; rt_copy_device copies it out."""
+    import rtamd
+    import torch
+    d = load_golden("hf40k")
+    renderer.upload(_scene(d))
+    renderer.set_params(d["params"])
+    w, h = int(d["w"]), int(d["h"])
+    full = renderer.render(w, h, depth=1)
+    nranks, nsets = 3, 2
+    sync_words = rtamd.frame_sync_words(nsets, nranks)
+    shm = rtamd.SharedAlloc(0, 4 * (nsets * h * w + sync_words))
+    side = torch.cuda.Stream()
+    s = side.cuda_stream
+    out = torch.full((nsets * h * w + sync_words,), -1, dtype=torch.int32, device="cuda")
+    rtamd.copy_device(out.data_ptr(), shm.ptr, out.numel() * 4, s)
+    torch.cuda.synchronize()
+    assert int(out.abs().sum().item()) == 0, "rt_shared_alloc memory is not zeroed"
+    hnd, off = rtamd.SharedFrames.export(0, shm.ptr)
+    assert len(hnd) == rtamd.SharedFrames.HANDLE_BYTES and off == 0
+    d_sync = shm.ptr + 4 * nsets * h * w
+    for use in range(2):   # each set filled twice: the second fill waits for the first present
+        for st in range(nsets):
+            for rank in range(nranks):
+                t = rtamd.rt_tiling(rank, nranks, 8, 0)
+                buf = torch.zeros(rtamd.tiling_pixels(w, h, rank, nranks, 8), dtype=torch.int32, device="cuda")
+                local = torch.zeros(nsets, dtype=torch.int32, device="cuda")
+                local[st] = use * buf.numel() // w   # this rank's block count of earlier uses
+                renderer.render_device(w, h, 1, 0, buf.data_ptr(), tiling=t, stream=s)
+                fs = rtamd.FrameSync(w, h, t, nranks, nsets, d_sync, local.data_ptr(), 2000)
+                fs.put(st, use, buf.data_ptr(), shm.ptr + 4 * st * h * w, s)
+                torch.cuda.synchronize()
+            fs.present(st, use, s)
+            torch.cuda.synchronize()
+            assert fs.status() == (0, use * nsets + st + 1)
+            got = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+            rtamd.copy_device(got.data_ptr(), shm.ptr + 4 * st * h * w, 4 * h * w, s)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), full), f"set {st} use {use}"
+    shm.close()
+
+
 def test_batched_band_assembly(renderer):
     """rt_assemble_bands_batch: three frames (different cameras) gathered as one batch per
     rank re-interleave to the three one-rank renders."""
