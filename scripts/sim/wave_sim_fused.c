@@ -1,0 +1,149 @@
+// Wave-level simulation of the tile kernel's traversal (8x8 tile per wave, Morton lanes,
+// ifif steps, wave-uniform prologue) for C3: counts vector quad requests by record kind and
+// by BFS rank of inner records.  Analysis only.
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { float mn[4], mx[4]; int32_t l, r, off, cnt; } node;
+static node* N; static int NN;
+static float* V; static int32_t* IDX; static int32_t* REF;
+static float P[32]; static float SMIN[3], SMAX[3];
+static int* bfs;   // inner node -> bfs rank (-1 for leaves)
+
+static void* rd(const char* f, size_t* n) {
+    FILE* fp = fopen(f, "rb"); fseek(fp, 0, SEEK_END); size_t s = ftell(fp); fseek(fp, 0, SEEK_SET);
+    void* p = malloc(s); fread(p, 1, s, fp); fclose(fp); if (n) *n = s; return p;
+}
+typedef struct { float x, y, z; } f3;
+static f3 v3(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static f3 sub(f3 a, f3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static f3 add(f3 a, f3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static f3 mul(f3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+static float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static f3 cross(f3 a, f3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static f3 nrm(f3 a) { float l = sqrtf(dot(a, a)); return l > 0 ? mul(a, 1.0f / l) : a; }
+
+typedef struct {
+    f3 o, d;
+    int stack[70]; int sc;   // stack[sc-1] = cur
+    int tk, tend;            // leaf state
+    float th; int res; int any; int done;
+} lane;
+
+static void lane_init(lane* L, f3 o, f3 d, int any) {
+    L->o = o; L->d = nrm(d); L->sc = 1; L->stack[0] = 0; L->th = 4294967296.0f; L->res = -1; L->any = any; L->done = 0;
+    L->tk = L->tend = 0;
+    if (N[0].l < 0) { L->tk = N[0].off; L->tend = N[0].off + N[0].cnt; }
+}
+static void slab(const lane* L, const node* b, float* tn, float* tf) {
+    float t0[3], t1[3];
+    const float* o = &L->o.x; const float* d = &L->d.x;
+    for (int k = 0; k < 3; ++k) { t0[k] = (b->mn[k] - o[k]) / d[k]; t1[k] = (b->mx[k] - o[k]) / d[k]; }
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = fminf(t0[k], t1[k]); hi[k] = fmaxf(t0[k], t1[k]); }
+    *tn = fmaxf(fmaxf(lo[0], lo[1]), lo[2]); *tf = fminf(fminf(hi[0], hi[1]), hi[2]);
+}
+// the record this lane fetches this iteration: >= 0 inner node id, < 0: -(tri ref + 1)
+static int lane_record(const lane* L) {
+    int cur = L->stack[L->sc - 1];
+    if (N[cur].l >= 0) return cur;
+    return -(L->tk + 1);
+}
+static void enter_top(lane* L) {
+    if (L->sc > 0) { int c = L->stack[L->sc - 1]; if (N[c].l < 0) { L->tk = N[c].off; L->tend = N[c].off + N[c].cnt; } }
+}
+static void lane_step(lane* L) {
+    int cur = L->stack[L->sc - 1];
+    const node* n = &N[cur];
+    if (n->l >= 0) {
+        float n0, f0, n1, f1;
+        slab(L, &N[n->l], &n0, &f0); slab(L, &N[n->r], &n1, &f1);
+        int i0 = n0 <= f0 && f0 >= 0.001f && n0 <= L->th, i1 = n1 <= f1 && f1 >= 0.001f && n1 <= L->th;
+        int a = n->l, b = n->r;
+        if (i0 && i1) { if (n0 > n1) { int t = a; a = b; b = t; } L->stack[L->sc - 1] = b; L->stack[L->sc++] = a; if (L->sc >= 65) { L->done = 1; L->sc = 0; return; } }
+        else if (i0) L->stack[L->sc - 1] = a;
+        else if (i1) L->stack[L->sc - 1] = b;
+        else L->sc--;
+        enter_top(L);
+    } else {
+        int stop = 0;
+        if (L->tk < L->tend) {
+            int t1 = REF[L->tk];
+            f3 a = v3(V[IDX[t1] * 4], V[IDX[t1] * 4 + 1], V[IDX[t1] * 4 + 2]);
+            f3 b = v3(V[IDX[t1 + 1] * 4], V[IDX[t1 + 1] * 4 + 1], V[IDX[t1 + 1] * 4 + 2]);
+            f3 c = v3(V[IDX[t1 + 2] * 4], V[IDX[t1 + 2] * 4 + 1], V[IDX[t1 + 2] * 4 + 2]);
+            f3 e1 = sub(b, a), e2 = sub(c, a), tv = sub(L->o, a), pv = cross(L->d, e2);
+            float det = 1.0f / dot(e1, pv); float u = dot(tv, pv) * det;
+            if (!(u < 0 || u > 1)) {
+                f3 qv = cross(tv, e1); float v = dot(L->d, qv) * det;
+                if (!(v < 0 || u + v > 1)) {
+                    float t = dot(e2, qv) * det;
+                    if (t < L->th && t > 0.001f) { L->th = t; L->res = t1; if (L->any) stop = 1; }
+                }
+            }
+        }
+        L->tk++;
+        if (stop) L->sc = 0;
+        else if (L->tk >= L->tend) { L->sc--; enter_top(L); }
+    }
+    if (L->sc == 0) L->done = 1;
+}
+
+
+static int lane_steps(lane* L) {   // steps of one lane's traversal to completion
+    int n = 0;
+    while (!L->done && L->sc > 0) { lane_step(L); ++n; }
+    return n;
+}
+int main() {
+    size_t s;
+    N = (node*)rd("c3_nodes.bin", &s); NN = (int)(s / sizeof(node));
+    V = (float*)rd("c3_vertices.bin", 0); IDX = (int32_t*)rd("c3_indices.bin", 0); REF = (int32_t*)rd("c3_tri_indices.bin", 0);
+    memcpy(P, rd("c3_params.bin", 0), 128); memcpy(SMIN, rd("c3_scene_min.bin", 0), 12); memcpy(SMAX, rd("c3_scene_max.bin", 0), 12);
+    bfs = malloc(sizeof(int) * NN); for (int i = 0; i < NN; ++i) bfs[i] = -1;
+    int* qq = malloc(sizeof(int) * NN); int h = 0, t = 0, rank = 0; qq[t++] = 0;
+    while (h < t) { int n = qq[h++]; if (N[n].l < 0) continue; bfs[n] = rank++; qq[t++] = N[n].l; qq[t++] = N[n].r; }
+    const int W = 1920, H = 1080;
+    f3 a = v3(P[0], P[1], P[2]), b = v3(P[4], P[5], P[6]), c = v3(P[8], P[9], P[10]), cam = v3(P[12], P[13], P[14]);
+    f3 light = v3(P[16], P[17], P[18]);
+    static lane L[64]; int act[64];
+    long long cur = 0, fused = 0, lanesum = 0, fused1 = 0;
+    for (int ty = 0; ty < H / 8; ++ty)
+        for (int tx = 0; tx < W / 8; ++tx) {
+            int P[64], S[64];
+            for (int l = 0; l < 64; ++l) {
+                int lx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4), ly = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
+                int x = tx * 8 + lx, y = ty * 8 + ly;
+                float xf = (float)((x - 0.5) / W), yf = (float)((y - 0.5) / H);
+                f3 ip = add(add(c, mul(a, xf)), mul(b, yf));
+                lane_init(&L[l], ip, sub(ip, cam), 0);
+                float tmin = -1e30f, tmax = 1e30f; int hit = 1;
+                const float* o = &L[l].o.x; const float* d = &L[l].d.x;
+                for (int k = 0; k < 3; ++k) { float i1 = (SMIN[k] - o[k]) / d[k], i2 = (SMAX[k] - o[k]) / d[k]; tmin = fmaxf(tmin, fminf(i1, i2)); tmax = fminf(tmax, fmaxf(i1, i2)); }
+                if (!(tmax >= tmin && tmax >= 0)) hit = 0;
+                P[l] = hit ? lane_steps(&L[l]) : 0;
+                S[l] = 0;
+                if (hit && L[l].res >= 0) {
+                    f3 hp = add(L[l].o, mul(L[l].d, L[l].th - 0.001f));
+                    f3 Ld = nrm(sub(light, hp));
+                    lane_init(&L[l], add(hp, mul(Ld, 0.001f)), Ld, 1);
+                    S[l] = lane_steps(&L[l]);
+                }
+            }
+            int mp = 0, ms = 0, mf = 0, mf1 = 0;
+            for (int l = 0; l < 64; ++l) {
+                if (P[l] > mp) mp = P[l];
+                if (S[l] > ms) ms = S[l];
+                if (P[l] + S[l] > mf) mf = P[l] + S[l];
+                if (P[l] + S[l] + (S[l] > 0) > mf1) mf1 = P[l] + S[l] + (S[l] > 0);
+                lanesum += P[l] + S[l];
+            }
+            cur += mp + ms; fused += mf; fused1 += mf1;
+        }
+    printf("wave iterations: phases %lld  fused %lld (%.3f)  fused+1 setup iteration %lld (%.3f); lane steps %lld; lane util phases %.3f fused %.3f\n",
+           cur, fused, (double)fused / cur, fused1, (double)fused1 / cur, lanesum, (double)lanesum / (64.0 * cur), (double)lanesum / (64.0 * fused));
+    return 0;
+}
