@@ -92,6 +92,9 @@ static void lane_step(lane* L) {
     if (L->sc == 0) L->done = 1;
 }
 
+// per-lane vector loads if a lane took its record from lane 0 of its quad / of its row of 16
+// when that lane is still traversing and fetches the same record (RTK_QSHARE 1 / 2)
+static long long ld_all = 0, ld_quad = 0, ld_row = 0, ld_both = 0;
 static long long q_vec = 0, q_vec_inner = 0, q_vec_tri = 0, lanes_vec = 0, iters = 0, iters_pro = 0;
 static long long q_rank[4];   // inner vector quad requests with bfs rank < 256, 512, 1024, 4096
 static const int KR[4] = {256, 512, 1024, 4096};
@@ -124,11 +127,22 @@ static void run_wave(lane* L, int* act) {
                 }
             }
         }
+        for (int i = 0; i < 64; ++i) {
+            if (rec[i] == 0x7fffffff) continue;
+            const int q0 = i & ~3, r0 = i & ~15;
+            const int sq = i != q0 && rec[q0] != 0x7fffffff && rec[q0] == rec[i];
+            const int sr = i != r0 && rec[r0] != 0x7fffffff && rec[r0] == rec[i];
+            ld_all++;
+            ld_quad += !sq;
+            ld_row += !sr;
+            ld_both += !sq && !sr;
+        }
         for (int i = 0; i < 64; ++i) if (act[i] && L[i].sc > 0) lane_step(&L[i]);
     }
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const int shadow = argc > 1 ? atoi(argv[1]) : 1;   // 0: primary rays only (C2)
     size_t s;
     N = (node*)rd("c3_nodes.bin", &s); NN = (int)(s / sizeof(node));
     V = (float*)rd("c3_vertices.bin", 0); IDX = (int32_t*)rd("c3_indices.bin", 0); REF = (int32_t*)rd("c3_tri_indices.bin", 0);
@@ -140,6 +154,7 @@ int main() {
     f3 a = v3(P[0], P[1], P[2]), b = v3(P[4], P[5], P[6]), c = v3(P[8], P[9], P[10]), cam = v3(P[12], P[13], P[14]);
     f3 light = v3(P[16], P[17], P[18]);
     static lane L[64]; int act[64];
+    long long waves_by_live[65] = {0}, it_primary = 0, pro_primary = 0;
     for (int ty = 0; ty < H / 8; ++ty)
         for (int tx = 0; tx < W / 8; ++tx) {
             for (int l = 0; l < 64; ++l) {
@@ -155,7 +170,11 @@ int main() {
                 if (!(tmax >= tmin && tmax >= 0)) hit = 0;
                 act[l] = hit;
             }
-            run_wave(L, act);
+            { int na = 0; for (int l = 0; l < 64; ++l) na += act[l]; waves_by_live[na]++; }
+            { const long long i0 = iters, p0 = iters_pro;
+              run_wave(L, act);
+              it_primary += iters - i0; pro_primary += iters_pro - p0; }
+            if (!shadow) continue;
             for (int l = 0; l < 64; ++l) {
                 int hit = act[l] && L[l].res >= 0;
                 act[l] = hit;
@@ -169,6 +188,11 @@ int main() {
         }
     printf("iters %lld prologue %lld  lane fetches(vec) %lld  quad req %lld (inner %lld tri %lld) lanes/qreq %.3f\n",
            iters, iters_pro, lanes_vec, q_vec, q_vec_inner, q_vec_tri, (double)lanes_vec / q_vec);
+    printf("  primary: %lld iterations + %lld prologue; shadow: %lld + %lld\n",
+           it_primary, pro_primary, iters - it_primary, iters_pro - pro_primary);
+    { long long part = 0; for (int k = 1; k < 64; ++k) part += waves_by_live[k];
+      printf("  tiles by lanes inside the scene box: none %lld, all 64 %lld, some %lld\n", waves_by_live[0], waves_by_live[64], part); }
+    printf("  vector lane loads: %lld; sharing with quad lane 0: %lld; with row lane 0: %lld; both: %lld\n", ld_all, ld_quad, ld_row, ld_both);
     for (int k = 0; k < 4; ++k) printf("  inner vector quad requests on bfs rank < %d: %lld (%.1f%% of all vector quad requests)\n", KR[k], q_rank[k], 100.0 * q_rank[k] / q_vec);
     return 0;
 }
