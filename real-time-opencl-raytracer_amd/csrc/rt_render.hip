@@ -45,9 +45,6 @@
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
 #endif
-#ifndef RTK_QSHARE
-#define RTK_QSHARE 0        // quad-shared record loads in the fast traversal (rt_kernel_body.inc)
-#endif
 
 namespace rtk {
 
