@@ -90,10 +90,12 @@ def parse_args(argv=None):
                          "taken when rank 0 saw it complete (ipc exchange)")
     ap.add_argument("--sync-timeout-ms", type=int, default=10000,
                     help="ipc exchange: bound on a put's wait for its frame set and on rank 0's wait for a frame")
-    ap.add_argument("--inject-fault", default="none", choices=["none", "wrong-bands", "drop-put"],
+    ap.add_argument("--inject-fault", default="none",
+                    choices=["none", "wrong-bands", "drop-put", "drop-put-warmup"],
                     help="test only (ipc exchange, N > 1): the last rank puts frame 4's bands from another frame's "
                          "buffer (wrong-bands: the frame check must fail), or skips its put of frame 4 (drop-put: "
-                         "frame delivery must fail by timeout)")
+                         "frame delivery must fail by timeout), or of frame 1, a warm-up frame (drop-put-warmup: "
+                         "the warm-up check must move every rank to the torch.distributed gather)")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="raise GPU_MAX_HW_QUEUES to at least this before HIP starts (frames in flight need a "
                          "hardware queue each, beside torch's and RCCL's streams); 0 = keep the inherited value")
@@ -387,6 +389,22 @@ def run(args, world, result_out=None):
     frames = torch_frames() if (rank == 0 and use_dist and not ipc) else None
     shared = None
     fsync = None
+    exchange_fallback = None
+
+    def drop_ipc():
+        """Every rank leaves the IPC band puts for the torch.distributed gather (B stays 1)."""
+        nonlocal ipc, tgather, shared, shm, fsync, frames, gbufs, glists
+        ipc, tgather, fsync = False, True, None
+        if shared is not None:
+            shared.close()
+            shared = None
+        if rank == 0:
+            if shm is not None:
+                shm.close()
+                shm = None
+            frames = torch_frames()
+            gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)]
+            glists = [list(g.unbind(0))[:world] for g in gbufs]
     if ipc:
         # rank 0's framebuffers (+ sync block) mapped into every rank (rt_ipc_export /
         # rt_ipc_open): each rank's bands go straight to their rows of rank 0's frame.  Only
@@ -419,17 +437,8 @@ def run(args, world, result_out=None):
         flag = torch.tensor([ok], device=dev)
         allreduce(flag, dist.ReduceOp.MIN)
         if flag.item() < 1.0:   # (B stays 1)
-            ipc, tgather = False, True
-            if shared is not None:
-                shared.close()
-                shared = None
-            if rank == 0:
-                if shm is not None:
-                    shm.close()
-                    shm = None
-                frames = torch_frames()
-                gbufs = [torch.zeros(shard_n, B * cap, dtype=torch.int32, device=dev) for _ in range(NB)]
-                glists = [list(g.unbind(0))[:world] for g in gbufs]
+            exchange_fallback = "frame mapping unavailable on some rank"
+            drop_ipc()
         else:
             put_dst = [[fr_base + 4 * (j * B + s) * h * w for s in range(B)] for j in range(NB)]
             sync_local = torch.zeros(NB, dtype=torch.int32, device=dev)   # this rank's per-set block counters
@@ -447,6 +456,7 @@ def run(args, world, result_out=None):
     # present saw it complete
     frame_of = [[-1] * B for _ in range(NB)]
     fault = args.inject_fault != "none" and rank == world - 1 and world > 1
+    fault_frame = 1 if args.inject_fault == "drop-put-warmup" else 4
     check_every = use_dist and rank == 0 and args.frame_check == "every"
     sums = torch.zeros(nframes + args.max_extra_warmup, dtype=torch.int64, device=dev) if check_every else None
     sums_ptr = sums.data_ptr() if sums is not None else 0
@@ -466,6 +476,40 @@ def run(args, world, result_out=None):
         return int((hv != -2).sum().item()), int((hv[:, 0, 0] != -2).sum().item())
 
     rays_f0, prim_f0 = count_rays(ptab[0])
+
+    # rank 0's frame checks: its own one-rank render of a camera, and every frame a buffer set
+    # holds against it (under --orbit every frame differs, so a band in the wrong frame shows)
+    L = ptab.shape[0]
+    sum_of = {}
+    if use_dist and rank == 0 and not args.shard:
+        full = torch.zeros(h * w, dtype=torch.int32, device=dev)
+        ref_sum = torch.zeros(1, dtype=torch.int64, device=dev)
+        got_frame = torch.zeros(h * w, dtype=torch.int32, device=dev)
+
+    def reference(cam):   # rank 0's one-rank frame of camera index cam into `full`; its checksum
+        r.set_params(ptab[cam])
+        r.render_device(w, h, depth, flags, full.data_ptr(), stream=streams[0].cuda_stream)
+        ref_sum.zero_()
+        rtamd.frame_checksum(full.data_ptr(), h * w, ref_sum.data_ptr(), streams[0].cuda_stream)
+        torch.cuda.synchronize(dev)
+        sum_of[cam] = int(ref_sum.item())
+        return sum_of[cam]
+
+    def check_held():
+        """(frames held, all equal): the frames rank 0's buffer sets hold vs reference()."""
+        torch.cuda.synchronize(dev)
+        held = [(j, s) for j in range(NB) for s in range(filled[j]) if frame_of[j][s] >= 0]
+        ok = bool(held)
+        for j, s in held:
+            reference(frame_of[j][s] % L)
+            if ipc:   # the uncached shared frame, copied out
+                rtamd.copy_device(got_frame.data_ptr(), put_dst[j][s], 4 * h * w, streams[0].cuda_stream)
+                torch.cuda.synchronize(dev)
+                got = got_frame
+            else:
+                got = frames[j][s]
+            ok = ok and bool(torch.equal(full, got))
+        return len(held), ok
 
     # One step = one frame: render this rank's bands -> (N > 1) RCCL gather of the bands to
     # rank 0 -> rank 0 re-interleaves them into the frame.
@@ -488,7 +532,10 @@ def run(args, world, result_out=None):
         fr_ptr = [f.data_ptr() for f in frames] if rank == 0 else [0] * NB
         # (--shard: the one-rank communicator assembles this rank's own bands only)
         slot_wait, xchg = comms[0].frame_exchanger(cap, w, cap // w if args.shard else h, args.band_rows)
-    if tgather:
+    pg = gopts = g_out = g_in = assemble = frame_ptr = gbuf_ptr = asm_stream = asm_sh = asm_done = None
+
+    def torch_gather_state():
+        nonlocal pg, gopts, g_out, g_in, assemble, frame_ptr, gbuf_ptr, asm_stream, asm_sh, asm_done
         pg = dist.distributed_c10d._get_default_group()
         gopts = dist.GatherOptions()
         gopts.rootRank = 0
@@ -502,6 +549,8 @@ def run(args, world, result_out=None):
             asm_stream = torch.cuda.Stream(dev)
             asm_sh = asm_stream.cuda_stream
             asm_done = [torch.cuda.Event() for _ in range(NB)]
+    if tgather:
+        torch_gather_state()
 
     def exchange(j, k, nfr):
         """Set j's batch (nfr frames, rendered on stream k = the current stream) to rank 0."""
@@ -510,8 +559,8 @@ def run(args, world, result_out=None):
             # rank 0 then waits (on this stream) until every rank's rows of the frame are in
             for s in range(nfr):
                 src = out_ptr[j][s]
-                if fault and frame_of[j][s] == 4:
-                    if args.inject_fault == "drop-put":
+                if fault and frame_of[j][s] == fault_frame:
+                    if args.inject_fault.startswith("drop-put"):
                         use[j] += 1
                         continue
                     src = out_ptr[(j + 1) % NB][s]   # another frame's bands
@@ -602,6 +651,39 @@ def run(args, world, result_out=None):
         drain()
     warmup_frames = args.warmup + extra
     torch.cuda.synchronize(dev)
+    # Warm-up check of the IPC exchange (N > 1): rank 0 saw every warm-up frame complete and
+    # the frames it holds equal its own one-rank renders.  If not (a peer path the one-GPU
+    # tests cannot exercise), every rank moves to the torch.distributed gather and warms up
+    # again, and the JSON names why (`band_exchange_fallback`).  Not under the timed-region
+    # faults of --inject-fault, which must surface.
+    if ipc and not args.shard and args.inject_fault in ("none", "drop-put-warmup"):
+        ok, why = 1.0, "a rank could not take part"
+        if rank == 0:
+            st, presented = fsync.status()
+            if st != 0 or presented != nstep[0]:
+                ok, why = 0.0, f"warm-up frame delivery: status {st}, {presented} of {nstep[0]} frames presented"
+            elif not check_held()[1]:
+                ok, why = 0.0, "a warm-up frame differs from rank 0's one-rank render"
+            r.set_params(ptab[0])
+        flag = torch.tensor([ok], device=dev)
+        allreduce(flag, dist.ReduceOp.MIN)
+        if flag.item() < 1.0:
+            exchange_fallback = why if rank == 0 else "rank 0 found the warm-up exchange failed"
+            print(f"rank {rank}: IPC band exchange failed its warm-up check ({exchange_fallback}); "
+                  "using torch.distributed", file=sys.stderr)
+            torch.cuda.synchronize(dev)
+            drop_ipc()
+            torch_gather_state()
+            pending[:] = [None] * NB
+            filled[:] = [0] * NB
+            asm_used[:] = [False] * NB
+            for fo in frame_of:
+                fo[:] = [-1] * B
+            for _ in range(args.warmup):
+                step()
+            drain()
+            warmup_frames += args.warmup
+            torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -624,7 +706,6 @@ def run(args, world, result_out=None):
     total_frames = warmup_frames + args.steps
     # frame n was rendered with camera n % L (the orbit table wraps when the time-based
     # warm-up ran past it; a static camera has L = 1)
-    L = ptab.shape[0]
     # rays of the timed frames (untimed: one aux render per distinct camera)
     if args.orbit:
         rays_local = prim_local = 0
@@ -654,31 +735,8 @@ def run(args, world, result_out=None):
     frame_ok = None
     frame_check = None
     if use_dist and rank == 0 and not args.shard:
-        full = torch.zeros(h * w, dtype=torch.int32, device=dev)
-        ref_sum = torch.zeros(1, dtype=torch.int64, device=dev)
-        sum_of = {}
-
-        def reference(cam):   # rank 0's one-rank frame of camera index cam into `full`; its checksum
-            r.set_params(ptab[cam])
-            r.render_device(w, h, depth, flags, full.data_ptr(), stream=streams[0].cuda_stream)
-            ref_sum.zero_()
-            rtamd.frame_checksum(full.data_ptr(), h * w, ref_sum.data_ptr(), streams[0].cuda_stream)
-            torch.cuda.synchronize(dev)
-            sum_of[cam] = int(ref_sum.item())
-            return sum_of[cam]
-
-        held = [(j, s) for j in range(NB) for s in range(filled[j]) if frame_of[j][s] >= 0]
-        frame_ok = bool(held)
-        got_frame = torch.zeros(h * w, dtype=torch.int32, device=dev)
-        for j, s in held:
-            reference(frame_of[j][s] % L)
-            if ipc:   # the uncached shared frame, copied out
-                rtamd.copy_device(got_frame.data_ptr(), put_dst[j][s], 4 * h * w, streams[0].cuda_stream)
-                torch.cuda.synchronize(dev)
-            else:
-                got_frame = frames[j][s]
-            frame_ok = frame_ok and bool(torch.equal(full, got_frame))
-        frame_check = {"held_frames_checked": len(held), "held_frames_equal": frame_ok,
+        held, frame_ok = check_held()
+        frame_check = {"held_frames_checked": held, "held_frames_equal": frame_ok,
                        "distinct_cameras": min(L, total_frames)}
         if check_every and sums is not None:
             got = sums[:total_frames].cpu().numpy()
@@ -939,6 +997,7 @@ def run(args, world, result_out=None):
                                           "(HIP IPC mapping, no collective)" if ipc
                                      else "torch.distributed gather (RCCL), B frames per gather, + rt_assemble_bands on rank 0's "
                                      "assembly stream"),
+                   "band_exchange_fallback": exchange_fallback,
                    "scene_distribution": (f"rank 0 builds; {scene_bytes} B scene image broadcast over RCCL "
                                           "(rt_scene_image_pack / _load)" if world > 1 else "single rank"),
                    "scene_setup_s": round(scene_s, 3),

@@ -527,7 +527,8 @@ __global__ void __launch_bounds__(256) bands_put_kernel(uint32_t* __restrict__ f
 //   [0] status (0 ok, 1 a put timed out waiting for its set, 2 a present timed out waiting
 //   for the puts), [1] frames presented, [2 .. 2+nsets) release[set] (uses of the set rank 0
 //   has presented), then arrive[set][rank] (uses of the set whose rows the rank has put).
-// Every wait is bounded (s_memrealtime, 100 MHz): a lost peer ends in a status, never a hang.
+// Every wait is bounded (s_memrealtime, 100 MHz): a lost peer ends in a status, never a hang;
+// after the first failed wait every later one returns at once (the status is sticky).
 constexpr uint32_t kSyncHead = 2;
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
@@ -553,7 +554,8 @@ __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restric
         if (use > 0) {
             const uint64_t t0 = now_ticks();
             while (sys_load(sync + kSyncHead + set) < use) {
-                if (now_ticks() - t0 > timeout_ticks) {
+                // once any wait has failed (status != 0) the exchange is over: no further wait
+                if (sys_load(sync) != 0u || now_ticks() - t0 > timeout_ticks) {
                     __hip_atomic_store(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     ab = 1;
                     break;
@@ -599,7 +601,7 @@ __global__ void __launch_bounds__(64) frame_present_kernel(uint32_t* sync, uint3
     bool ok = true;
     for (uint32_t r = lane; r < nranks; r += 64) {
         while (sys_load(sync + kSyncHead + nsets + set * nranks + r) < use + 1u) {
-            if (now_ticks() - t0 > timeout_ticks) { ok = false; break; }
+            if (sys_load(sync) != 0u || now_ticks() - t0 > timeout_ticks) { ok = false; break; }
             __builtin_amdgcn_s_sleep(2);
         }
     }

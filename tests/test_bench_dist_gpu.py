@@ -96,3 +96,16 @@ def test_frame_delivery_fails_when_a_rank_drops_a_frame():
     p = _ranks_on_one_gpu(2, ["--steps", "6", "--sync-timeout-ms", "300", "--inject-fault", "drop-put"])
     assert p.returncode != 0
     assert "frame delivery failed" in p.stderr
+
+
+def test_failed_warmup_exchange_falls_back_to_the_rccl_gather():
+    """The last rank never puts warm-up frame 1: the warm-up check (rank 0's delivery status
+    and held frames) moves every rank to the torch.distributed gather before the timed frames,
+    which then assemble correctly; the JSON names the fallback."""
+    p = _ranks_on_one_gpu(2, ["--steps", "6", "--warmup", "4", "--sync-timeout-ms", "300", "--orbit", "0.01",
+                              "--inject-fault", "drop-put-warmup"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert "warm-up frame delivery" in res["config"]["band_exchange_fallback"]
+    assert "torch.distributed gather" in res["config"]["band_exchange"]
+    assert res["config"]["gathered_frame_equals_single_rank_render"] is True
