@@ -45,9 +45,6 @@
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
 #endif
-#ifndef RTK_QCOOP
-#define RTK_QCOOP 0         // quad-cooperative record fetch in the fast traversal (A/B)
-#endif
 
 namespace rtk {
 
