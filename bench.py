@@ -398,6 +398,7 @@ def run(args, world, result_out=None):
         if shared is not None:
             shared.close()
             shared = None
+        dist.barrier()   # every peer has unmapped rank 0's frames before rank 0 frees them
         if rank == 0:
             if shm is not None:
                 shm.close()

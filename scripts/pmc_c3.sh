@@ -2,7 +2,8 @@
 # Separate rocprofv3 --pmc passes (counters only, no trace domains) over a short
 # bench.py run, then the median-per-dispatch summary of the render kernel.
 # Usage: [BENCH_ARGS="--config c5"] scripts/pmc_c3.sh [outdir] ["COUNTER SET 1" "COUNTER SET 2" ...]
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$ROOT}" || exit 1
 export GPU_MAX_HW_QUEUES=16
 out=${1:-gpurun_out/pmc}; shift
 if [ $# -eq 0 ]; then

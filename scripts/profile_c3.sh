@@ -5,7 +5,8 @@
 # process runs with the same queue count as an unprofiled bench.py (which raises it itself).
 # Outputs under gpurun_out/prof_*; summarise with scripts/profile_summary.py.
 # Usage: scripts/profile_c3.sh [bench args...]   (default: the C3 headline)
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$ROOT}" || exit 1
 export GPU_MAX_HW_QUEUES=16
 mkdir -p gpurun_out
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- \

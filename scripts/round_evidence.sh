@@ -6,7 +6,7 @@
 # Each GPU step has its own time limit; a fatal step ends the call (scripts/gpu_steps.sh).
 # Usage: scripts/round_evidence.sh ROUND   (e.g. r03)
 rnd=${1:?round}
-cd "$GRAFT_REPO_ROOT" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 scripts/gpu_steps.sh \
   "pytest_gpu|420|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" \
