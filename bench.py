@@ -91,11 +91,14 @@ def parse_args(argv=None):
     ap.add_argument("--sync-timeout-ms", type=int, default=10000,
                     help="ipc exchange: bound on a put's wait for its frame set and on rank 0's wait for a frame")
     ap.add_argument("--inject-fault", default="none",
-                    choices=["none", "wrong-bands", "drop-put", "drop-put-warmup"],
+                    choices=["none", "wrong-bands", "drop-put", "drop-put-warmup", "no-peer", "open-fails"],
                     help="test only (ipc exchange, N > 1): the last rank puts frame 4's bands from another frame's "
                          "buffer (wrong-bands: the frame check must fail), or skips its put of frame 4 (drop-put: "
                          "frame delivery must fail by timeout), or of frame 1, a warm-up frame (drop-put-warmup: "
-                         "the warm-up check must move every rank to the torch.distributed gather)")
+                         "the warm-up check must move every rank to the torch.distributed gather); or, at set-up, "
+                         "its peer-access check says no (no-peer) or it maps rank 0's frames from a corrupted "
+                         "handle, so rt_ipc_open fails (open-fails): every rank must take the torch.distributed "
+                         "gather")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="raise GPU_MAX_HW_QUEUES to at least this before HIP starts (frames in flight need a "
                          "hardware queue each, beside torch's and RCCL's streams); 0 = keep the inherited value")
@@ -413,6 +416,7 @@ def run(args, world, result_out=None):
         # cannot map them, every rank falls back to the torch.distributed gather.
         store = dist.distributed_c10d._get_default_store()
         ok = 1.0
+        setup_fault = args.inject_fault if (rank == world - 1 and world > 1) else "none"
         try:
             if rank == 0:
                 try:
@@ -428,9 +432,13 @@ def run(args, world, result_out=None):
                 if len(blob) != rtamd.SharedFrames.HANDLE_BYTES + 12:
                     raise rtamd.RtError(-2, "rank 0 could not export its frames")
                 dev0 = int.from_bytes(blob[-4:], "little")
-                if not rtamd.peer_access(local, dev0):
-                    raise rtamd.RtError(-2, f"device {local} cannot access rank 0's device {dev0} (no peer access)")
-                shared = rtamd.SharedFrames.open(local, blob[:-12], int.from_bytes(blob[-12:-4], "little"))
+                if not rtamd.peer_access(local, dev0) or setup_fault == "no-peer":
+                    raise rtamd.RtError(-2, f"device {local} cannot access rank 0's device {dev0} (no peer access"
+                                            + (", injected" if setup_fault == "no-peer" else "") + ")")
+                handle = blob[:-12]
+                if setup_fault == "open-fails":   # a handle naming no allocation: hipIpcOpenMemHandle fails
+                    handle = bytes(len(handle))
+                shared = rtamd.SharedFrames.open(local, handle, int.from_bytes(blob[-12:-4], "little"))
                 fr_base = shared.ptr
         except rtamd.RtError as e:
             print(f"rank {rank}: frame mapping unavailable ({e}); using torch.distributed", file=sys.stderr)
@@ -461,6 +469,7 @@ def run(args, world, result_out=None):
     check_every = use_dist and rank == 0 and args.frame_check == "every"
     sums = torch.zeros(nframes + args.max_extra_warmup, dtype=torch.int64, device=dev) if check_every else None
     sums_ptr = sums.data_ptr() if sums is not None else 0
+    checksummed = []   # frame indices whose checksum was taken at their present (ipc exchange only)
 
     # rays traced by this rank in a frame with params p (counted with the aux planes, untimed)
     d = max(depth, 1)
@@ -569,7 +578,10 @@ def run(args, world, result_out=None):
                 if rank == 0:   # the set goes back to the ranks after its consumer (the checksum)
                     fsync.present(j, use[j], sh[k], release=not check_every)
                     if check_every:
-                        rtamd.frame_checksum(put_dst[j][s], h * w, sums_ptr + 8 * frame_of[j][s], sh[k])
+                        n = frame_of[j][s]
+                        if n < sums.numel():
+                            rtamd.frame_checksum(put_dst[j][s], h * w, sums_ptr + 8 * n, sh[k])
+                            checksummed.append(n)
                         fsync.release(j, use[j], sh[k])
                 use[j] += 1
             return
@@ -680,6 +692,7 @@ def run(args, world, result_out=None):
             asm_used[:] = [False] * NB
             for fo in frame_of:
                 fo[:] = [-1] * B
+            checksummed.clear()   # the failed IPC warm-up's checksums are not frames of this run's check
             for _ in range(args.warmup):
                 step()
             drain()
@@ -740,10 +753,12 @@ def run(args, world, result_out=None):
         frame_check = {"held_frames_checked": held, "held_frames_equal": frame_ok,
                        "distinct_cameras": min(L, total_frames)}
         if check_every and sums is not None:
-            got = sums[:total_frames].cpu().numpy()
-            bad = [n for n in range(total_frames) if int(got[n]) != sum_of.get(n % L, None) and
+            # only the frames presented over IPC carry a checksum (after a fall-back to the RCCL
+            # gather no further checksums are taken)
+            got = sums.cpu().numpy()
+            bad = [n for n in checksummed if int(got[n]) != sum_of.get(n % L, None) and
                    int(got[n]) != reference(n % L)]
-            frame_check.update({"presented_frames_checksummed": total_frames, "checksum_mismatches": len(bad)})
+            frame_check.update({"presented_frames_checksummed": len(checksummed), "checksum_mismatches": len(bad)})
             frame_ok = frame_ok and not bad
         r.set_params(ptab[0])
 

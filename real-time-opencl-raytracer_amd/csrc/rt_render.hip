@@ -142,6 +142,15 @@ __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int&
     }
 }
 
+// The same range as byte offsets of the records in the fast traversal's allocation
+// (triangle records after the inner records, 48 B each): [tk, tend).
+__device__ __forceinline__ void leaf_bytes(const DevScene& S, uint32_t ref, uint32_t& tk, uint32_t& tend) {
+    int off, cnt;
+    leaf_range(S, ref, off, cnt);
+    tk = S.tri_off + (uint32_t)off * 48u;
+    tend = tk + (uint32_t)cnt * 48u;
+}
+
 struct Stack {
     uint32_t* lds;      // this lane's column: lds[i * 64]
     uint32_t* glb;      // this pixel's column: glb[(i - kLdsStack) * gstride]
@@ -534,6 +543,13 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// The first failure's code is kept: a later wait that returns early because the status is
+// already set does not overwrite it (compare-and-swap from 0).
+__device__ __forceinline__ void set_status(uint32_t* sync, uint32_t code) {
+    uint32_t expect = 0u;
+    __hip_atomic_compare_exchange_strong(sync, &expect, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // rt_bands_put_sync: one block per local row.  Before writing set `set` for its use `use`
 // the block waits until rank 0 has presented the set's previous use (back-pressure: a peer
@@ -556,7 +572,7 @@ __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restric
             while (sys_load(sync + kSyncHead + set) < use) {
                 // once any wait has failed (status != 0) the exchange is over: no further wait
                 if (sys_load(sync) != 0u || now_ticks() - t0 > timeout_ticks) {
-                    __hip_atomic_store(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    set_status(sync, 1u);
                     ab = 1;
                     break;
                 }
@@ -608,7 +624,7 @@ __global__ void __launch_bounds__(64) frame_present_kernel(uint32_t* sync, uint3
     const bool all_ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
     if (lane == 0) {
         if (!all_ok) {
-            __hip_atomic_store(sync, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            set_status(sync, 2u);
             return;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -723,6 +739,11 @@ struct rt_ctx {
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
     struct { bool on = false; unsigned long long* d_counts = nullptr; } trace;   // rt_fetch_counts
+    // rt_render's row groups: one stream (so one frame slot) and one "rendered" event per group
+    hipStream_t gstream[8] = {};
+    hipEvent_t gdone[8] = {};
+    hipEvent_t gstart = nullptr;
+    std::vector<FrameSlot*> last_group;   // the slots of the last grouped rt_render
     bool timing_valid = false;
     std::string err;
 };
@@ -1056,6 +1077,12 @@ int rt_destroy(rt_ctx* c) {
     for (auto& f : c->ring)
         for (hipEvent_t& e : f.e)
             if (e) (void)hipEventDestroy(e);
+    for (int g = 0; g < 8; ++g) {
+        if (c->gstream[g]) (void)hipStreamSynchronize(c->gstream[g]);
+        if (c->gdone[g]) (void)hipEventDestroy(c->gdone[g]);
+        if (c->gstream[g]) (void)hipStreamDestroy(c->gstream[g]);
+    }
+    if (c->gstart) (void)hipEventDestroy(c->gstart);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -1355,6 +1382,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     if ((rc = slot_for(c, (void*)s, &Lp))) return rc;
     rt_ctx::FrameSlot& L = *Lp;
     c->last_slot = &L;
+    c->last_group.clear();
     const int math = (flags & RT_FLAG_STRICT_MATH) ? 0 : (flags & RT_FLAG_HW_MATH) ? 1 : 2;
 
     rtk::Frame F;
@@ -1557,31 +1585,92 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     return RT_OK;
 }
 
+// rt_render's overlap of the frame's readback with its rendering (raytrace_gpgpu renders the
+// whole frame, then reads it back: RayTracer.cpp:330-344).  A frame of at least
+// kGroupMinPixels is cut into RTK_RENDER_GROUPS groups of contiguous rows (rt_tiling with one
+// band per "rank", so a group's rows are one contiguous run of the frame and of its aux
+// planes), each rendered straight into its part of the frame buffer on its own stream (its
+// own frame slot and longest-first order); a group's rows go to the host as soon as it is
+// done, while the next groups render.  RTK_RENDER_CHAIN 1: the groups render one after
+// another (each stream waits for the previous group's kernels), so the first rows finish
+// first; 0: concurrently.  The pixels are the same as one whole-frame launch's (a pixel's
+// arithmetic does not depend on how the frame is cut: DESIGN.md 5).
+#ifndef RTK_RENDER_GROUPS
+#define RTK_RENDER_GROUPS 4
+#endif
+#ifndef RTK_RENDER_CHAIN
+#define RTK_RENDER_CHAIN 1
+#endif
+static_assert(RTK_RENDER_GROUPS >= 1 && RTK_RENDER_GROUPS <= 8, "rt_render groups: 1..8 streams");
+constexpr uint64_t kGroupMinPixels = 512 * 512;
+
 int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr,
               const rt_aux* aux) {
     if (!c || !out_bgr) return set_err(c, "rt_render: invalid argument", RT_ERR_INVALID_ARG);
+    if (w == 0 || h == 0 || depth < 0 || depth > RT_MAX_DEPTH) return set_err(c, "rt_render: invalid argument", RT_ERR_INVALID_ARG);
     const size_t npix = (size_t)w * h;
     HIPC(c, hipSetDevice(c->device));
     int rc = ensure(c, c->d_out, c->out_cap, npix);
     if (rc) return rc;
     rt_aux dev{nullptr, nullptr, nullptr};
     const bool want = aux && (aux->hits || aux->t || aux->rgb);
+    const size_t dd = (size_t)std::max(depth, 1);
     if (want) {
-        size_t d = (size_t)std::max(depth, 1);
-        if ((rc = ensure(c, c->d_hits, c->hits_cap, npix * d * 2))) return rc;
-        if ((rc = ensure(c, c->d_t, c->t_cap, npix * d))) return rc;
+        if ((rc = ensure(c, c->d_hits, c->hits_cap, npix * dd * 2))) return rc;
+        if ((rc = ensure(c, c->d_t, c->t_cap, npix * dd))) return rc;
         if ((rc = ensure(c, c->d_rgb, c->rgb_cap, npix * 3))) return rc;
         dev = rt_aux{c->d_hits, c->d_t, c->d_rgb};
     }
-    rc = rt_render_device(c, w, h, depth, flags, nullptr, c->d_out, want ? &dev : nullptr, c->stream);
-    if (rc) return rc;
-    HIPC(c, hipMemcpyAsync(out_bgr, c->d_out, npix * 4, hipMemcpyDeviceToHost, c->stream));
-    if (want) {
-        if (aux->hits) HIPC(c, hipMemcpyAsync(aux->hits, c->d_hits, npix * depth * 2 * 4, hipMemcpyDeviceToHost, c->stream));
-        if (aux->t) HIPC(c, hipMemcpyAsync(aux->t, c->d_t, npix * depth * 4, hipMemcpyDeviceToHost, c->stream));
-        if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb, c->d_rgb, npix * 3 * 4, hipMemcpyDeviceToHost, c->stream));
+    // the group's rows: band_rows a multiple of the 16-row block, at most one band per group
+    uint32_t groups = npix >= kGroupMinPixels ? RTK_RENDER_GROUPS : 1;
+    const uint32_t band_rows = ((h + groups - 1) / groups + 15u) & ~15u;
+    groups = (h + band_rows - 1) / band_rows;
+    if (groups <= 1) {
+        rc = rt_render_device(c, w, h, depth, flags, nullptr, c->d_out, want ? &dev : nullptr, c->stream);
+        if (rc) return rc;
+        HIPC(c, hipMemcpyAsync(out_bgr, c->d_out, npix * 4, hipMemcpyDeviceToHost, c->stream));
+        if (want) {
+            if (aux->hits) HIPC(c, hipMemcpyAsync(aux->hits, c->d_hits, npix * depth * 2 * 4, hipMemcpyDeviceToHost, c->stream));
+            if (aux->t) HIPC(c, hipMemcpyAsync(aux->t, c->d_t, npix * depth * 4, hipMemcpyDeviceToHost, c->stream));
+            if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb, c->d_rgb, npix * 3 * 4, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIPC(c, hipStreamSynchronize(c->stream));
+        return RT_OK;
     }
-    HIPC(c, hipStreamSynchronize(c->stream));
+    for (uint32_t g = 0; g < groups; ++g) {
+        if (!c->gstream[g]) HIPC(c, hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking));
+        if (!c->gdone[g]) HIPC(c, hipEventCreateWithFlags(&c->gdone[g], hipEventDisableTiming));
+    }
+    // after whatever the ctx's own stream still holds (the synchronous entry points leave it idle)
+    if (!c->gstart) HIPC(c, hipEventCreateWithFlags(&c->gstart, hipEventDisableTiming));
+    HIPC(c, hipEventRecord(c->gstart, c->stream));
+    std::vector<rt_ctx::FrameSlot*> slots;
+    // every group's kernels first, then the readbacks in group order: a copy into pageable
+    // memory may block the host until it is done, and the later groups must already be queued
+    for (uint32_t g = 0; g < groups; ++g) {
+        hipStream_t s = c->gstream[g];
+        HIPC(c, hipStreamWaitEvent(s, RTK_RENDER_CHAIN && g ? c->gdone[g - 1] : c->gstart, 0));
+        const rt_tiling t{(int32_t)g, (int32_t)groups, (int32_t)band_rows, 0};
+        const size_t p0 = (size_t)g * band_rows * w;
+        rt_aux ga{nullptr, nullptr, nullptr};
+        if (want) ga = rt_aux{c->d_hits + p0 * dd * 2, c->d_t + p0 * dd, c->d_rgb + p0 * 3};
+        rc = rt_render_device(c, w, h, depth, flags, &t, c->d_out + p0, want ? &ga : nullptr, s);
+        if (rc) return rc;
+        slots.push_back(c->last_slot);
+        if (RTK_RENDER_CHAIN) HIPC(c, hipEventRecord(c->gdone[g], s));
+    }
+    for (uint32_t g = 0; g < groups; ++g) {
+        hipStream_t s = c->gstream[g];
+        const size_t p0 = (size_t)g * band_rows * w, np = (size_t)std::min<uint64_t>(band_rows, h - (uint64_t)g * band_rows) * w;
+        HIPC(c, hipMemcpyAsync(out_bgr + p0, c->d_out + p0, np * 4, hipMemcpyDeviceToHost, s));
+        if (want) {
+            if (aux->hits) HIPC(c, hipMemcpyAsync(aux->hits + p0 * depth * 2, c->d_hits + p0 * depth * 2, np * depth * 2 * 4, hipMemcpyDeviceToHost, s));
+            if (aux->t) HIPC(c, hipMemcpyAsync(aux->t + p0 * depth, c->d_t + p0 * depth, np * depth * 4, hipMemcpyDeviceToHost, s));
+            if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb + p0 * 3, c->d_rgb + p0 * 3, np * 3 * 4, hipMemcpyDeviceToHost, s));
+        }
+    }
+    for (uint32_t g = 0; g < groups; ++g) HIPC(c, hipStreamSynchronize(c->gstream[g]));
+    c->last_group = slots;
     return RT_OK;
 }
 
@@ -1625,11 +1714,17 @@ int rt_timing_average(rt_ctx* c, int32_t n, float* total_ms, float* traverse_ms)
 int rt_last_deferred(rt_ctx* c, uint32_t* count) {
     if (!c || !count) return RT_ERR_INVALID_ARG;
     *count = 0;
-    rt_ctx::FrameSlot* L = c->last_slot;
-    if (!L || !L->d_wcnt || L->nframe == 0) return RT_OK;
-    HIPC(c, hipEventSynchronize(L->idle));
-    const uint64_t par = (L->nframe - 1) & 1u;   // the last frame's parity set
-    HIPC(c, hipMemcpy(count, L->d_wcnt + par * L->wcnt_set + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    // the last frame: one slot, or every row group of the last grouped rt_render
+    std::vector<rt_ctx::FrameSlot*> ls = c->last_group;
+    if (ls.empty()) ls.push_back(c->last_slot);
+    for (rt_ctx::FrameSlot* L : ls) {
+        if (!L || !L->d_wcnt || L->nframe == 0) continue;
+        HIPC(c, hipEventSynchronize(L->idle));
+        const uint64_t par = (L->nframe - 1) & 1u;   // the last frame's parity set
+        uint32_t v = 0;
+        HIPC(c, hipMemcpy(&v, L->d_wcnt + par * L->wcnt_set + kRestartSlot, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        *count += v;
+    }
     return RT_OK;
 }
 

@@ -155,6 +155,7 @@ int main(int argc, char** argv) {
     f3 light = v3(P[16], P[17], P[18]);
     static lane L[64]; int act[64];
     long long waves_by_live[65] = {0}, it_primary = 0, pro_primary = 0;
+    static int wave_len[(1920 / 8) * (1080 / 8)]; int nwl = 0;   // per active wave: primary + shadow iterations
     for (int ty = 0; ty < H / 8; ++ty)
         for (int tx = 0; tx < W / 8; ++tx) {
             for (int l = 0; l < 64; ++l) {
@@ -171,10 +172,11 @@ int main(int argc, char** argv) {
                 act[l] = hit;
             }
             { int na = 0; for (int l = 0; l < 64; ++l) na += act[l]; waves_by_live[na]++; }
+            const long long w0 = iters + iters_pro;
             { const long long i0 = iters, p0 = iters_pro;
               run_wave(L, act);
               it_primary += iters - i0; pro_primary += iters_pro - p0; }
-            if (!shadow) continue;
+            if (!shadow) { if (iters + iters_pro > w0) wave_len[nwl++] = (int)(iters + iters_pro - w0); continue; }
             for (int l = 0; l < 64; ++l) {
                 int hit = act[l] && L[l].res >= 0;
                 act[l] = hit;
@@ -185,7 +187,16 @@ int main(int argc, char** argv) {
                 }
             }
             run_wave(L, act);
+            if (iters + iters_pro > w0) wave_len[nwl++] = (int)(iters + iters_pro - w0);
         }
+    {   // distribution of a wave's dependent iterations (prologue + main loop): the chain each wave runs
+        int cmp(const void* x, const void* y) { return *(const int*)x - *(const int*)y; }
+        qsort(wave_len, nwl, sizeof(int), cmp);
+        long long sum = 0; for (int i = 0; i < nwl; ++i) sum += wave_len[i];
+        printf("waves with work %d: iterations per wave mean %.1f p50 %d p90 %d p99 %d p99.9 %d max %d\n", nwl,
+               (double)sum / nwl, wave_len[nwl / 2], wave_len[nwl * 9 / 10], wave_len[nwl * 99 / 100],
+               wave_len[nwl * 999 / 1000], wave_len[nwl - 1]);
+    }
     printf("iters %lld prologue %lld  lane fetches(vec) %lld  quad req %lld (inner %lld tri %lld) lanes/qreq %.3f\n",
            iters, iters_pro, lanes_vec, q_vec, q_vec_inner, q_vec_tri, (double)lanes_vec / q_vec);
     printf("  primary: %lld iterations + %lld prologue; shadow: %lld + %lld\n",

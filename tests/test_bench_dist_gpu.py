@@ -109,3 +109,20 @@ def test_failed_warmup_exchange_falls_back_to_the_rccl_gather():
     assert "warm-up frame delivery" in res["config"]["band_exchange_fallback"]
     assert "torch.distributed gather" in res["config"]["band_exchange"]
     assert res["config"]["gathered_frame_equals_single_rank_render"] is True
+
+
+@pytest.mark.parametrize("fault,why", [("no-peer", "no peer access"), ("open-fails", "hipIpcOpenMemHandle")])
+def test_unmappable_frames_fall_back_to_the_rccl_gather(fault, why):
+    """The set-up half of the exchange's fallback (bench.py: peer-access gate + rt_ipc_open):
+    the last rank's peer-access check says no, or it maps rank 0's frames from a handle that
+    names no allocation (rt_ipc_open returns an error).  Every rank must agree to use the
+    torch.distributed gather, name the reason, and its frames must equal the one-rank
+    renders of an orbiting camera (every frame differs)."""
+    p = _ranks_on_one_gpu(2, ["--steps", "8", "--orbit", "0.01", "--inject-fault", fault])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert why in p.stderr, p.stderr[-2000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["config"]["band_exchange_fallback"] == "frame mapping unavailable on some rank"
+    assert "torch.distributed gather" in res["config"]["band_exchange"]
+    assert res["config"]["frame_check"]["held_frames_checked"] > 0
+    assert res["config"]["gathered_frame_equals_single_rank_render"] is True

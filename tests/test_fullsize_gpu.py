@@ -123,6 +123,26 @@ def test_default_math_matches_reference_kernel(renderer, name, tmp_path):
         assert np.array_equal(d1["t"][:, 0].view(np.uint32), d3["t"][:, 0].view(np.uint32))
         if not cfg["flags"] & 1:   # with the shadow ray: the same shadow hits
             assert np.array_equal(d1["hits"][:, 0, 1], d3["hits"][:, 0, 1])
+        if not cfg["flags"] & 1:
+            _pin_depth1_pixels(name, d3, d1["out"], ref)
+
+
+def _pin_depth1_pixels(label, d3, out1, ref):
+    """The benched depth-1 pixels themselves against the reference kernel.  The reference
+    always traces RAY_TRACE_DEPTH = 3 bounces (volumeRender.cl:12), but a pixel whose reflected
+    ray misses ends with ray_depth = 1, and its packed colour is then color / 1 * shadow / 1
+    (volumeRender.cl:1519-1546): exactly the depth-1 frame's.  So on every pixel where the
+    pinned depth-3 frame stopped after its first hit (or its primary ray missed: black in
+    both) the depth-1 frame must equal the reference kernel's packed pixel."""
+    h0, h1 = d3["hits"][:, 0, 0], d3["hits"][:, 1, 0]
+    one_hit = (h0 >= 0) & (h1 < 0)
+    subset = one_hit | (h0 < 0)
+    nd = int(np.sum(out1[subset] != ref[subset]))
+    print(f"{label}: S_ref depth-1 frame vs reference kernel on {int(one_hit.sum())} one-hit pixels "
+          f"(+{int((h0 < 0).sum())} primary misses) of {out1.size}: {nd} differ")
+    assert nd == 0
+    if label.startswith(("c3", "c4")):   # terrain: most reflected rays leave the scene (C1's room keeps them)
+        assert one_hit.sum() > 0.5 * (h0 >= 0).sum(), "the subset covers most of the scene's pixels"
 
 
 @pytest.mark.parametrize("nranks", [2, 4, 8])
@@ -150,3 +170,8 @@ def test_c4_default_math_shards_match_reference_kernel(renderer, tmp_path):
     renderer.set_params(params)
     out = _banded(renderer, w, h, 3, 0, 8)
     assert int(np.sum(out != ref)) == 0
+    # the benched depth-1 arithmetic, as the same 8 assembled shards, on the pixels whose
+    # depth-3 trace stopped after one hit
+    d3 = renderer.render(w, h, depth=3, aux=True)
+    assert np.array_equal(d3["out"], ref)
+    _pin_depth1_pixels("c4 (8 shards)", d3, _banded(renderer, w, h, 1, 0, 8), ref)
