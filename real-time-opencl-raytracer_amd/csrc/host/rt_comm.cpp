@@ -201,7 +201,11 @@ int rt_ipc_open(int32_t device, const uint8_t* handle, int32_t handle_bytes, voi
     hipIpcMemHandle_t h;
     std::memcpy(&h, handle, sizeof h);
     const hipError_t e = hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) return comm_err(std::string("rt_ipc_open: hipIpcOpenMemHandle: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    if (e != hipSuccess) {
+        *d_ptr = nullptr;
+        (void)hipGetLastError();   // the failure is reported here; later calls must not see it as theirs
+        return comm_err(std::string("rt_ipc_open: hipIpcOpenMemHandle: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+    }
     return RT_OK;
 }
 

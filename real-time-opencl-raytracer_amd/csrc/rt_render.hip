@@ -939,6 +939,7 @@ int rt_assemble_bands_batch(uint32_t* d_frame, const uint32_t* d_slots, uint64_t
         return set_err(nullptr, "rt_assemble_bands: slot_pixels smaller than rank 0's bands", RT_ERR_INVALID_ARG);
     if (((uintptr_t)d_frame | (uintptr_t)d_slots) & 15u)
         return set_err(nullptr, "rt_assemble_bands: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
+    (void)hipGetLastError();   // an earlier call's error is not this launch's
     hipLaunchKernelGGL(rtk::assemble_bands_kernel, dim3(h, nframes), dim3(256), 0, (hipStream_t)stream, d_frame, d_slots,
                        slot_pixels, frame_pixels, w, h, (uint32_t)nranks, (uint32_t)band_rows);
     hipError_t e = hipGetLastError();
@@ -963,6 +964,7 @@ int rt_bands_put(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_
     if ((w & 3u) == 0 && (((uintptr_t)d_frame | (uintptr_t)d_bands) & 15u))
         return set_err(nullptr, "rt_bands_put: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
     const uint32_t local_rows = (uint32_t)(npix / w);
+    (void)hipGetLastError();   // an earlier call's error is not this launch's
     hipLaunchKernelGGL(rtk::bands_put_kernel, dim3(local_rows), dim3(256), 0, (hipStream_t)stream, d_frame, d_bands, w,
                        local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows);
     hipError_t e = hipGetLastError();
@@ -991,6 +993,7 @@ int rt_bands_put_sync(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, ui
     if ((w & 3u) == 0 && (((uintptr_t)d_frame | (uintptr_t)d_bands) & 15u))
         return set_err(nullptr, "rt_bands_put_sync: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
     const uint32_t local_rows = (uint32_t)(npix / w);
+    (void)hipGetLastError();   // an earlier call's error is not this launch's
     hipLaunchKernelGGL(rtk::bands_put_sync_kernel, dim3(local_rows), dim3(256), 0, (hipStream_t)stream, d_frame, d_bands,
                        w, local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows, d_sync, d_local,
                        (uint32_t)nsets, (uint32_t)set, use, timeout_ticks(timeout_ms));
@@ -1003,6 +1006,7 @@ int rt_frame_present(uint32_t* d_sync, int32_t nsets, int32_t set, uint32_t use,
                      int32_t release, void* stream) {
     if (!d_sync || nsets < 1 || set < 0 || set >= nsets || nranks < 1)
         return set_err(nullptr, "rt_frame_present: invalid argument", RT_ERR_INVALID_ARG);
+    (void)hipGetLastError();   // an earlier call's error is not this launch's
     hipLaunchKernelGGL(rtk::frame_present_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_sync, (uint32_t)nsets,
                        (uint32_t)set, use, (uint32_t)nranks, timeout_ticks(timeout_ms), release ? 1u : 0u);
     hipError_t e = hipGetLastError();
@@ -1013,6 +1017,7 @@ int rt_frame_present(uint32_t* d_sync, int32_t nsets, int32_t set, uint32_t use,
 int rt_frame_release(uint32_t* d_sync, int32_t nsets, int32_t set, uint32_t use, void* stream) {
     if (!d_sync || nsets < 1 || set < 0 || set >= nsets)
         return set_err(nullptr, "rt_frame_release: invalid argument", RT_ERR_INVALID_ARG);
+    (void)hipGetLastError();   // an earlier call's error is not this launch's
     hipLaunchKernelGGL(rtk::frame_release_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_sync, (uint32_t)set, use);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(nullptr, std::string("rt_frame_release: ") + hipGetErrorString(e), RT_ERR_DEVICE);
@@ -1032,6 +1037,7 @@ int rt_frame_sync_status(const uint32_t* d_sync, uint32_t* status, uint32_t* pre
 int rt_frame_checksum(const uint32_t* d_frame, uint64_t pixels, uint64_t* d_sum, void* stream) {
     if (!d_frame || !d_sum || pixels == 0) return set_err(nullptr, "rt_frame_checksum: invalid argument", RT_ERR_INVALID_ARG);
     const uint64_t blocks = std::min<uint64_t>(1024, (pixels + 255) / 256);
+    (void)hipGetLastError();   // an earlier call's error is not this launch's
     hipLaunchKernelGGL(rtk::frame_checksum_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, d_frame,
                        pixels, (unsigned long long*)d_sum);
     hipError_t e = hipGetLastError();
@@ -1499,6 +1505,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const dim3 grid(F.num_blocks), block(256);
     int ax = aux ? 1 : 0;
     HIPC(c, hipEventRecord(E.e[0], s));
+    (void)hipGetLastError();   // the launches below are checked with hipGetLastError: not an earlier call's error
 
     // The frame's first kernel zeroes the other parity set for the next frame: from then on
     // the next frame on this slot must use that set, even if a later launch of this frame
@@ -1599,7 +1606,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
 #define RTK_RENDER_GROUPS 4
 #endif
 #ifndef RTK_RENDER_CHAIN
-#define RTK_RENDER_CHAIN 1
+#define RTK_RENDER_CHAIN 0
+#endif
+#ifndef RTK_RENDER_PRIO
+#define RTK_RENDER_PRIO 0    // 1: the first group's stream gets the device's highest priority
 #endif
 static_assert(RTK_RENDER_GROUPS >= 1 && RTK_RENDER_GROUPS <= 8, "rt_render groups: 1..8 streams");
 constexpr uint64_t kGroupMinPixels = 512 * 512;
@@ -1638,7 +1648,11 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         return RT_OK;
     }
     for (uint32_t g = 0; g < groups; ++g) {
-        if (!c->gstream[g]) HIPC(c, hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking));
+        if (!c->gstream[g]) {
+            int lo = 0, hi = 0;
+            if (RTK_RENDER_PRIO) HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPC(c, hipStreamCreateWithPriority(&c->gstream[g], hipStreamNonBlocking, g == 0 ? hi : lo));
+        }
         if (!c->gdone[g]) HIPC(c, hipEventCreateWithFlags(&c->gdone[g], hipEventDisableTiming));
     }
     // after whatever the ctx's own stream still holds (the synchronous entry points leave it idle)

@@ -52,6 +52,13 @@ def test_bench_dist_shard_diagnostic_completes(gather):
     assert res["value"] > 0 and "shard 0/8" in res["config"]["parallelism"]
 
 
+def _why(p):
+    """The part of a failed run's stderr that says why: from its last traceback, else the tail."""
+    err = p.stderr
+    i = err.rfind("Traceback (most recent call last)")
+    return err[i:i + 3000] if i >= 0 else err[-3000:]
+
+
 def _ranks_on_one_gpu(n, extra, timeout=115):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
@@ -119,8 +126,8 @@ def test_unmappable_frames_fall_back_to_the_rccl_gather(fault, why):
     torch.distributed gather, name the reason, and its frames must equal the one-rank
     renders of an orbiting camera (every frame differs)."""
     p = _ranks_on_one_gpu(2, ["--steps", "8", "--orbit", "0.01", "--inject-fault", fault])
-    assert p.returncode == 0, p.stderr[-2000:]
-    assert why in p.stderr, p.stderr[-2000:]
+    assert p.returncode == 0, _why(p)
+    assert why in p.stderr, p.stderr[-3000:]
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["config"]["band_exchange_fallback"] == "frame mapping unavailable on some rank"
     assert "torch.distributed gather" in res["config"]["band_exchange"]

@@ -605,3 +605,35 @@ def test_latency_and_gather_roofs_measure(renderer):
     assert ms4 <= ms1 * 1.05 and ms64 <= ms1 * 1.05
     pk_ms, pk_n = renderer.gather_peak(16384, 256)
     assert pk_ms > 0 and pk_n > 0
+
+
+def test_triangle_records_beyond_2_to_the_24(renderer):
+    """A leaf whose triangle records lie at index >= 2^24 of the record array: the fast
+    traversal addresses them by byte offset (tk, a 32-bit byte cursor), so scenes of more than
+    16.8 M triangle references render the same triangles as small ones.  The knot fixture's
+    reference array gets 2^24 + 5 padding entries in front (every leaf range shifted past
+    them, about 0.8 GB of triangle records, still one allocation): its depth-1 frames (the
+    benched first_bounce_kernel with its offset select) and depth-3 frames equal the unpadded
+    scene's in every mode, and the S_strict frame equals the oracle's."""
+    d = load_golden("knot16k")
+    w, h = int(d["w"]), int(d["h"])
+    base = _scene(d)
+    renderer.upload(base)
+    renderer.set_params(d["params"])
+    want = {(dep, m): renderer.render(w, h, depth=dep, flags=f, aux=True) for dep in (1, 3) for m, f in MODES.items()}
+    pad = (1 << 24) + 5
+    big = _scene(d)
+    big.tri_indices = np.concatenate([np.full(pad, base.tri_indices[0], np.int32), base.tri_indices])
+    big.nodes = big.nodes.copy()   # (from_arrays may share the fixture's arrays)
+    ni = big.nodes.view(np.int32)
+    leaf = ni[:, 8] < 0
+    ni[leaf, 10] += pad
+    renderer.upload(big)
+    renderer.set_params(d["params"])
+    try:
+        for (dep, m), ref in want.items():
+            got = renderer.render(w, h, depth=dep, flags=MODES[m], aux=True)
+            _compare(got, ref, f"padded refs, depth {dep}, {m}")
+        _compare(renderer.render(w, h, depth=3, flags=STRICT, aux=True), _oracle(d, 3), "padded refs vs oracle")
+    finally:
+        renderer.upload(base)
