@@ -42,6 +42,18 @@
 
 #include "rt_abi.h"
 
+#ifndef RTK_TRI2
+#define RTK_TRI2 0          // 1: a lane in a leaf loads and tests two of its triangles per iteration
+#endif
+#ifndef RTK_T2
+#define RTK_T2 0            // 1: two-level inner records (a node's child boxes + its children's child boxes)
+#endif
+#ifndef RTK_WF_WAVES
+#define RTK_WF_WAVES 7      // waves per SIMD the wavefront kernels are bounded to
+#endif
+#ifndef RTK_FB_WAVES
+#define RTK_FB_WAVES 8      // waves per SIMD the S_ref depth-1 kernel is bounded to
+#endif
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
 #endif
@@ -56,6 +68,12 @@ constexpr uint32_t kCntEscape = 31u;
 constexpr int kLdsStack = RTK_LDS_STACK;
 constexpr int kGlobalStack = 64 - kLdsStack;         // slots kLdsStack..63
 constexpr uint32_t kBlockPx = 16;                    // a block = 2 x 2 tiles of 8 x 8 pixels
+// Inner record: {child boxes x3, {r0, r1, ..}} = 4 float4 (64 B); RTK_T2 (A/B): + the left
+// and the right child's own child boxes and refs, 11 float4 (176 B):
+//   [0..2] child boxes, [3] {r0, r1, left's r0, left's r1}, [4..6] left's child boxes,
+//   [7..9] right's child boxes, [10] {right's r0, right's r1, 0, 0}
+constexpr uint32_t kInnerF4 = RTK_T2 ? 11u : 4u;
+constexpr uint32_t kInnerBytes = kInnerF4 * 16u;
 
 struct DevScene {
     const float4* __restrict__ wnodes;   // [n_inner][4]
@@ -175,7 +193,7 @@ struct Stack {
 // wave-distinct, [6] wave iterations, [7] mixed iterations; stride 256 (one block's lanes).
 // vmem = false: a record the wave read once through the scalar cache (the traversal's
 // wave-uniform prologue): a lane fetch and a wave-distinct record, but no quad request.
-__device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id, bool vmem = true) {
+__device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id, bool vmem = true, bool iter = true) {
     const uint64_t act = __builtin_amdgcn_read_exec();
     const int lane = (int)(threadIdx.x & 63u);
     bool quad_first = true, wave_first = true;
@@ -191,7 +209,7 @@ __device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id
     fc[t * 256] += 1u;
     fc[(2 + t) * 256] += (vmem && quad_first) ? 1u : 0u;
     fc[(4 + t) * 256] += wave_first ? 1u : 0u;
-    if (lane == (int)__builtin_ctzll(act)) {
+    if (iter && lane == (int)__builtin_ctzll(act)) {   // (iter false: a second record of the same iteration)
         fc[6 * 256] += 1u;
         fc[7 * 256] += (lm != 0 && (act & ~lm) != 0) ? 1u : 0u;
     }
@@ -1192,13 +1210,13 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             }
         }
     }
-    std::vector<float4> wn((size_t)std::max(n_inner, 1) * 4, make_float4(0, 0, 0, 0));
+    std::vector<float4> wn((size_t)std::max(n_inner, 1) * rtk::kInnerF4, make_float4(0, 0, 0, 0));
     bool fast_ok = true;  // slab-test fast quotient domain (rt_kernel_body.inc axis_ok)
     for (int32_t n = 0; n < nn; ++n) {
         if (inner_id[n] < 0) continue;
         const rt_bvh_node& L = nodes[nodes[n].offset_left];
         const rt_bvh_node& R = nodes[nodes[n].offset_right];
-        float4* q = &wn[(size_t)inner_id[n] * 4];
+        float4* q = &wn[(size_t)inner_id[n] * rtk::kInnerF4];
         // axis-major: {L.min, R.min, L.max, R.max} per axis (rt_kernel_body.inc slab2_pk)
         q[0] = make_float4(L.min.x, R.min.x, L.max.x, R.max.x);
         q[1] = make_float4(L.min.y, R.min.y, L.max.y, R.max.y);
@@ -1208,6 +1226,24 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         std::memcpy(&f0, &r0, 4);
         std::memcpy(&f1, &r1, 4);
         q[3] = make_float4(f0, f1, 0.0f, 0.0f);
+        if (RTK_T2) {   // each inner child's own child boxes and refs (its record's [0..3])
+            for (int side = 0; side < 2; ++side) {
+                const int32_t ch = side ? nodes[n].offset_right : nodes[n].offset_left;
+                if (inner_id[ch] < 0) continue;
+                const rt_bvh_node& cl = nodes[nodes[ch].offset_left];
+                const rt_bvh_node& cr = nodes[nodes[ch].offset_right];
+                float4* g = q + 4 + 3 * side;
+                g[0] = make_float4(cl.min.x, cr.min.x, cl.max.x, cr.max.x);
+                g[1] = make_float4(cl.min.y, cr.min.y, cl.max.y, cr.max.y);
+                g[2] = make_float4(cl.min.z, cr.min.z, cl.max.z, cr.max.z);
+                uint32_t g0 = ref_of[nodes[ch].offset_left], g1 = ref_of[nodes[ch].offset_right];
+                float h0, h1;
+                std::memcpy(&h0, &g0, 4);
+                std::memcpy(&h1, &g1, 4);
+                if (side) q[10] = make_float4(h0, h1, 0.0f, 0.0f);
+                else { q[3].z = h0; q[3].w = h1; }
+            }
+        }
         for (int k = 0; k < 3; ++k) {
             const float* qf = &q[k].x;
             for (int j = 0; j < 4; ++j) {

@@ -55,9 +55,12 @@ static int lane_record(const lane* L) {
 static void enter_top(lane* L) {
     if (L->sc > 0) { int c = L->stack[L->sc - 1]; if (N[c].l < 0) { L->tk = N[c].off; L->tend = N[c].off + N[c].cnt; } }
 }
+static int T2 = 0, TT2 = 0;   // TT2=1: two triangles of one leaf per iteration   // env T2=1: an inner step that descends into an inner child runs that child's step too
+static int descended;  // set by lane_step: this inner step moved cur to a child (push or advance)
 static void lane_step(lane* L) {
     int cur = L->stack[L->sc - 1];
     const node* n = &N[cur];
+    descended = 0;
     if (n->l >= 0) {
         float n0, f0, n1, f1;
         slab(L, &N[n->l], &n0, &f0); slab(L, &N[n->r], &n1, &f1);
@@ -67,6 +70,7 @@ static void lane_step(lane* L) {
         else if (i0) L->stack[L->sc - 1] = a;
         else if (i1) L->stack[L->sc - 1] = b;
         else L->sc--;
+        descended = (i0 || i1) && L->sc > 0;
         enter_top(L);
     } else {
         int stop = 0;
@@ -98,6 +102,7 @@ static long long ld_all = 0, ld_quad = 0, ld_row = 0, ld_both = 0;
 static long long q_vec = 0, q_vec_inner = 0, q_vec_tri = 0, lanes_vec = 0, iters = 0, iters_pro = 0;
 static long long q_rank[4];   // inner vector quad requests with bfs rank < 256, 512, 1024, 4096
 static const int KR[4] = {256, 512, 1024, 4096};
+static long long t2_second = 0, lane_steps = 0;   // every lane step of the main loop and the prologue
 
 static void run_wave(lane* L, int* act) {
     // prologue: while all active lanes sit on the same inner node
@@ -106,7 +111,7 @@ static void run_wave(lane* L, int* act) {
         for (int i = 0; i < 64; ++i) if (act[i] && L[i].sc > 0) { any = 1; int c = L[i].stack[L[i].sc - 1]; if (first < 0) first = c; else if (c != first) uni = 0; }
         if (!any || !uni || N[first].l < 0) break;
         iters_pro++;
-        for (int i = 0; i < 64; ++i) if (act[i] && L[i].sc > 0) lane_step(&L[i]);
+        for (int i = 0; i < 64; ++i) if (act[i] && L[i].sc > 0) { lane_step(&L[i]); lane_steps++; }
     }
     for (;;) {
         int any = 0;
@@ -137,12 +142,19 @@ static void run_wave(lane* L, int* act) {
             ld_row += !sr;
             ld_both += !sq && !sr;
         }
-        for (int i = 0; i < 64; ++i) if (act[i] && L[i].sc > 0) lane_step(&L[i]);
+        for (int i = 0; i < 64; ++i) if (act[i] && L[i].sc > 0) {
+            lane_step(&L[i]); lane_steps++;
+            if (T2 && descended && L[i].sc > 0 && N[L[i].stack[L[i].sc - 1]].l >= 0) { lane_step(&L[i]); t2_second++; }
+            else if (TT2 && rec[i] < 0 && L[i].sc > 0 && N[L[i].stack[L[i].sc - 1]].l < 0 && L[i].tk < L[i].tend &&
+                     lane_record(&L[i]) == rec[i] - 1) { lane_step(&L[i]); t2_second++; }   // the leaf's next triangle
+        }
     }
 }
 
 int main(int argc, char** argv) {
     const int shadow = argc > 1 ? atoi(argv[1]) : 1;   // 0: primary rays only (C2)
+    T2 = getenv("T2") ? atoi(getenv("T2")) : 0;
+    TT2 = getenv("TT2") ? atoi(getenv("TT2")) : 0;
     size_t s;
     N = (node*)rd("c3_nodes.bin", &s); NN = (int)(s / sizeof(node));
     V = (float*)rd("c3_vertices.bin", 0); IDX = (int32_t*)rd("c3_indices.bin", 0); REF = (int32_t*)rd("c3_tri_indices.bin", 0);
@@ -197,6 +209,9 @@ int main(int argc, char** argv) {
                (double)sum / nwl, wave_len[nwl / 2], wave_len[nwl * 9 / 10], wave_len[nwl * 99 / 100],
                wave_len[nwl * 999 / 1000], wave_len[nwl - 1]);
     }
+    printf("lane steps %lld: lane utilisation of the wave iterations %.3f\n", lane_steps,
+           (double)lane_steps / (64.0 * (double)(iters + iters_pro)));
+    if (T2 || TT2) printf("T2: second inner steps taken without a fetch: %lld\n", t2_second);
     printf("iters %lld prologue %lld  lane fetches(vec) %lld  quad req %lld (inner %lld tri %lld) lanes/qreq %.3f\n",
            iters, iters_pro, lanes_vec, q_vec, q_vec_inner, q_vec_tri, (double)lanes_vec / q_vec);
     printf("  primary: %lld iterations + %lld prologue; shadow: %lld + %lld\n",
