@@ -969,6 +969,9 @@ def run(args, world, result_out=None):
             pj = json.load(open(pmc_files[-1]))
             lib_now = rtamd.library_digest()
             roof["traffic"] = pj.get("hbm_bytes_per_launch")
+            if pj.get("occupancy"):   # achieved waves per SIMD of the same kernel (PMC, separate run)
+                roof["occupancy"] = dict(pj["occupancy"], file=os.path.relpath(pmc_files[-1], ROOT),
+                                         stale=pj.get("library_digest") != rtamd.library_digest())
             roof["traffic_source"] = {
                 "file": os.path.relpath(pmc_files[-1], ROOT),
                 "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command (separate runs, not this "

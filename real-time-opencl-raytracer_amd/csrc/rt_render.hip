@@ -734,6 +734,7 @@ struct rt_ctx {
     // stream are ordered by it and share one slot.
     struct FrameSlot {
         void* stream = nullptr;
+        uint64_t tkey = 0;                                                  // the tiling it renders (0: whole frame)
         uint64_t last_use = 0;
         hipEvent_t idle = nullptr;                                          // recorded after each frame
         uint64_t nframe = 0;                                                // frames rendered on this slot
@@ -807,15 +808,16 @@ static void free_slot(rt_ctx::FrameSlot& f) {
 // The frame scratch of `stream` (created on first use; beyond kMaxSlots streams the
 // least recently used slot is recycled once its last frame has finished -- waited on
 // through the slot's own event, the stream itself may be gone by then).
-static int slot_for(rt_ctx* c, void* stream, rt_ctx::FrameSlot** out) {
+static int slot_for(rt_ctx* c, void* stream, uint64_t tkey, rt_ctx::FrameSlot** out) {
     ++c->slot_clock;
     for (auto& f : c->slots)
-        if (f.stream == stream) { f.last_use = c->slot_clock; *out = &f; return RT_OK; }
+        if (f.stream == stream && f.tkey == tkey) { f.last_use = c->slot_clock; *out = &f; return RT_OK; }
     if ((int)c->slots.size() < rt_ctx::kMaxSlots) {
         c->slots.reserve(rt_ctx::kMaxSlots);   // slot pointers stay valid
         c->slots.emplace_back();
         rt_ctx::FrameSlot& f = c->slots.back();
         f.stream = stream;
+        f.tkey = tkey;
         f.last_use = c->slot_clock;
         HIPC(c, hipEventCreateWithFlags(&f.idle, hipEventDisableTiming));
         *out = &f;
@@ -826,6 +828,7 @@ static int slot_for(rt_ctx* c, void* stream, rt_ctx::FrameSlot** out) {
         if (f.last_use < lru->last_use) lru = &f;
     HIPC(c, hipEventSynchronize(lru->idle));
     lru->stream = stream;
+    lru->tkey = tkey;
     lru->cost_key = 0;
     lru->cost_ready = false;
     lru->last_use = c->slot_clock;
@@ -1421,7 +1424,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     int rc = RT_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     rt_ctx::FrameSlot* Lp = nullptr;
-    if ((rc = slot_for(c, (void*)s, &Lp))) return rc;
+    // a slot per (stream, tiling): one stream may render several tilings in turn (rt_render's row
+    // groups), each with its own longest-first order
+    const uint64_t tkey = T->nranks > 1 ? ((uint64_t)(uint32_t)T->rank << 40) ^ ((uint64_t)(uint32_t)T->nranks << 20) ^
+                                              (uint64_t)(uint32_t)T->band_rows ^ (1ull << 63)
+                                        : 0;
+    if ((rc = slot_for(c, (void*)s, tkey, &Lp))) return rc;
     rt_ctx::FrameSlot& L = *Lp;
     c->last_slot = &L;
     c->last_group.clear();
@@ -1647,7 +1655,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
 #ifndef RTK_RENDER_PRIO
 #define RTK_RENDER_PRIO 0    // 1: the first group's stream gets the device's highest priority
 #endif
-static_assert(RTK_RENDER_GROUPS >= 1 && RTK_RENDER_GROUPS <= 8, "rt_render groups: 1..8 streams");
+static_assert(RTK_RENDER_GROUPS >= 1 && RTK_RENDER_GROUPS + (RTK_RENDER_CHAIN == 2) <= 8, "rt_render: at most 8 streams");
 constexpr uint64_t kGroupMinPixels = 512 * 512;
 
 int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr,
@@ -1683,7 +1691,10 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         HIPC(c, hipStreamSynchronize(c->stream));
         return RT_OK;
     }
-    for (uint32_t g = 0; g < groups; ++g) {
+    // streams: group g's readback (and, unless RTK_RENDER_CHAIN 2, its kernels) on gstream[g];
+    // RTK_RENDER_CHAIN 2: every group's kernels one after another on gstream[groups]
+    const bool one_render_stream = RTK_RENDER_CHAIN == 2;
+    for (uint32_t g = 0; g < groups + (one_render_stream ? 1u : 0u); ++g) {
         if (!c->gstream[g]) {
             int lo = 0, hi = 0;
             if (RTK_RENDER_PRIO) HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1698,8 +1709,9 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
     // every group's kernels first, then the readbacks in group order: a copy into pageable
     // memory may block the host until it is done, and the later groups must already be queued
     for (uint32_t g = 0; g < groups; ++g) {
-        hipStream_t s = c->gstream[g];
-        HIPC(c, hipStreamWaitEvent(s, RTK_RENDER_CHAIN && g ? c->gdone[g - 1] : c->gstart, 0));
+        hipStream_t s = c->gstream[one_render_stream ? groups : g];
+        if (!one_render_stream || g == 0)
+            HIPC(c, hipStreamWaitEvent(s, RTK_RENDER_CHAIN == 1 && g ? c->gdone[g - 1] : c->gstart, 0));
         const rt_tiling t{(int32_t)g, (int32_t)groups, (int32_t)band_rows, 0};
         const size_t p0 = (size_t)g * band_rows * w;
         rt_aux ga{nullptr, nullptr, nullptr};
@@ -1708,6 +1720,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         if (rc) return rc;
         slots.push_back(c->last_slot);
         if (RTK_RENDER_CHAIN) HIPC(c, hipEventRecord(c->gdone[g], s));
+        if (one_render_stream) HIPC(c, hipStreamWaitEvent(c->gstream[g], c->gdone[g], 0));
     }
     for (uint32_t g = 0; g < groups; ++g) {
         hipStream_t s = c->gstream[g];
@@ -1719,7 +1732,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
             if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb + p0 * 3, c->d_rgb + p0 * 3, np * 3 * 4, hipMemcpyDeviceToHost, s));
         }
     }
-    for (uint32_t g = 0; g < groups; ++g) HIPC(c, hipStreamSynchronize(c->gstream[g]));
+    for (uint32_t g = 0; g < groups + (one_render_stream ? 1u : 0u); ++g) HIPC(c, hipStreamSynchronize(c->gstream[g]));
     c->last_group = slots;
     return RT_OK;
 }

@@ -4,7 +4,11 @@ and writes profiles/<round>/pmc_<config>.json (HBM bytes per render-kernel launc
 FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B/lane reads,
 MI355X_MICROARCH.md HBM section); FETCH_SIZE / WRITE_SIZE are in kB = 1024 B.
 
-    python scripts/profile_summary.py r02 [c3]
+    python scripts/profile_summary.py r02 [c3] [--occupancy PMC_JSON]
+
+--occupancy: a per-kernel summary of scripts/pmc_configs.sh (MeanOccupancyPerCU pass of the
+same kernel, one frame in flight): its achieved waves per SIMD go into pmc_<config>.json, which
+bench.py reports in roofline.occupancy.
 """
 import csv
 import glob
@@ -27,8 +31,14 @@ def counter(d, name):
 
 
 def main():
-    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
+    args = sys.argv[1:]
+    occ = None
+    if "--occupancy" in args:
+        i = args.index("--occupancy")
+        occ = json.load(open(args[i + 1]))
+        args = args[:i] + args[i + 2:]
+    rnd = args[0] if len(args) > 0 else "r01"
+    cfg = args[1] if len(args) > 1 else "c3"
     out = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(out, exist_ok=True)
     stats = glob.glob(os.path.join(ROOT, "gpurun_out", "prof_trace", "**", "*kernel_stats.csv"), recursive=True)[0]
@@ -77,6 +87,16 @@ def main():
         "library_digest": hashlib.sha256(open(os.path.join(ROOT, "real-time-opencl-raytracer_amd", "lib",
                                                              "librtamd.so"), "rb").read()).hexdigest()[:16],
     }
+    if occ is not None:
+        d = occ["derived"]
+        res["occupancy"] = {
+            "waves_per_simd": round(d["waves_per_simd"], 3) if "waves_per_simd" in d else None,
+            "waves_per_simd_active_cu": round(d["waves_per_simd_active_cu"], 3) if "waves_per_simd_active_cu" in d else None,
+            "max_waves_per_simd": 8,
+            "kernel": occ["kernel"],
+            "source": "rocprofv3 --pmc MeanOccupancyPerCU / MeanOccupancyPerActiveCU (SQ_LEVEL_WAVES accumulated over "
+                      "GRBM_GUI_ACTIVE per CU, rocprofiler-sdk counter_defs.yaml for gfx950) / 4 SIMDs, one frame in "
+                      "flight (scripts/pmc_configs.sh)"}
     json.dump(res, open(os.path.join(out, f"pmc_{cfg}.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
