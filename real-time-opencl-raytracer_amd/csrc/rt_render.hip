@@ -1655,6 +1655,9 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
 #ifndef RTK_RENDER_PRIO
 #define RTK_RENDER_PRIO 0    // 1: the first group's stream gets the device's highest priority
 #endif
+#ifndef RTK_RENDER_ZC
+#define RTK_RENDER_ZC 0      // 1: pinned, device-mapped host memory is rendered into directly (no readback)
+#endif
 static_assert(RTK_RENDER_GROUPS >= 1 && RTK_RENDER_GROUPS + (RTK_RENDER_CHAIN == 2) <= 8, "rt_render: at most 8 streams");
 constexpr uint64_t kGroupMinPixels = 512 * 512;
 
@@ -1674,6 +1677,19 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         if ((rc = ensure(c, c->d_t, c->t_cap, npix * dd))) return rc;
         if ((rc = ensure(c, c->d_rgb, c->rgb_cap, npix * 3))) return rc;
         dev = rt_aux{c->d_hits, c->d_t, c->d_rgb};
+    }
+    if (RTK_RENDER_ZC && !want) {
+        // the caller's buffer is pinned host memory the device can write (hipHostMalloc, or
+        // registered as mapped): the kernel's pixel stores go straight to it over the host link
+        // while the frame renders, with no readback after it
+        hipPointerAttribute_t pa;
+        if (hipPointerGetAttributes(&pa, out_bgr) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer) {
+            rc = rt_render_device(c, w, h, depth, flags, nullptr, (uint32_t*)pa.devicePointer, nullptr, c->stream);
+            if (rc) return rc;
+            HIPC(c, hipStreamSynchronize(c->stream));
+            return RT_OK;
+        }
+        (void)hipGetLastError();   // pageable memory: not an error, the readback path below
     }
     // the group's rows: band_rows a multiple of the 16-row block, at most one band per group
     uint32_t groups = npix >= kGroupMinPixels ? RTK_RENDER_GROUPS : 1;

@@ -8,11 +8,16 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$ROOT}" || exit 1
 export GPU_MAX_HW_QUEUES=16
 out=$1; cfgs=$2; shift 2
-sets=("MeanOccupancyPerCU" "MeanOccupancyPerActiveCU" "FETCH_SIZE" "WRITE_SIZE"
-      "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES"
-      "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM"
-      "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum"
-      "GRBM_GUI_ACTIVE TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum")
+# PMC_SETS=occ: only the two occupancy passes
+if [ "${PMC_SETS:-all}" = occ ]; then
+  sets=("MeanOccupancyPerCU" "MeanOccupancyPerActiveCU")
+else
+  sets=("MeanOccupancyPerCU" "MeanOccupancyPerActiveCU" "FETCH_SIZE" "WRITE_SIZE"
+        "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES"
+        "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM"
+        "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum"
+        "GRBM_GUI_ACTIVE TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum")
+fi
 for c in $cfgs; do
   i=0; mkdir -p "$out/$c"
   for set in "${sets[@]}"; do

@@ -5,7 +5,7 @@ cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out/r04
 scripts/gpu_steps.sh \
  "dist_fallback|200|python -u -m pytest tests/test_bench_dist_gpu.py -x -q -k 'unmappable or warmup' --timeout 150 --timeout-method thread" \
- "hb|420|scripts/ab_host_boundary.sh 'main g1 g3p g4pr g6p g8p g8pr g4s g6s g3s' c3 2 300" \
+ "hb|500|scripts/ab_host_boundary.sh 'main g1 zc4 zc1 g3p g4pr g6p g8p g8pr g4s g6s g3s' c3 2 300" \
  "tri2_parity|300|RTAMD_LIB=\$PWD/real-time-opencl-raytracer_amd/lib/ab/tri2/librtamd.so python -u -m pytest tests/test_render_gpu.py tests/test_reference_pin_gpu.py -x -q --timeout 150 --timeout-method thread" \
  "t2_parity|300|RTAMD_LIB=\$PWD/real-time-opencl-raytracer_amd/lib/ab/t2/librtamd.so python -u -m pytest tests/test_render_gpu.py tests/test_reference_pin_gpu.py -x -q --timeout 150 --timeout-method thread" \
  "ab_tri2|500|scripts/ab_bench.sh 'main tri2 tri2w7 t2 t2w6' 'c2 c3' 2" \

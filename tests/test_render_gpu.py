@@ -637,3 +637,39 @@ def test_triangle_records_beyond_2_to_the_24(renderer):
         _compare(renderer.render(w, h, depth=3, flags=STRICT, aux=True), _oracle(d, 3), "padded refs vs oracle")
     finally:
         renderer.upload(base)
+
+
+def test_render_readback_paths_agree(renderer):
+    """rt_render (the reference's synchronous boundary, raytrace_gpgpu) on a frame large enough
+    for its row groups (>= 512 x 512): into pageable memory (row groups read back while later
+    groups render), into pinned host memory, with aux planes, and via rt_render_device -- the
+    same pixels, and the aux planes equal a one-launch device render's."""
+    import torch
+    d = load_golden("knot16k")
+    renderer.upload(_scene(d))
+    w, h = 1024, 720
+    p = d["params"].copy()
+    renderer.set_params(p)
+    dev = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    renderer.render_device(w, h, 1, 0, dev.data_ptr(), stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    want = dev.cpu().numpy().view(np.uint32)
+    pageable = np.zeros(w * h, np.uint32)
+    renderer.render_host_ptr(w, h, 1, 0, pageable.ctypes.data)
+    pinned = torch.zeros(w * h, dtype=torch.int32, pin_memory=True)
+    renderer.render_host_ptr(w, h, 1, 0, pinned.data_ptr())
+    assert np.array_equal(pageable, want)
+    assert np.array_equal(pinned.numpy().view(np.uint32), want)
+    for depth, flags in ((1, 0), (3, STRICT), (3, WAVEFRONT | WF_SORT)):
+        a = renderer.render(w, h, depth=depth, flags=flags, aux=True)   # rt_render, row groups
+        hits = torch.zeros(w * h * depth * 2, dtype=torch.int32, device="cuda")
+        tt = torch.zeros(w * h * depth, dtype=torch.float32, device="cuda")
+        rgb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+        renderer.render_device(w, h, depth, flags, dev.data_ptr(), stream=s.cuda_stream,
+                               aux_ptrs=(hits.data_ptr(), tt.data_ptr(), rgb.data_ptr()))
+        torch.cuda.synchronize()
+        assert np.array_equal(a["out"], dev.cpu().numpy().view(np.uint32)), (depth, flags)
+        assert np.array_equal(a["hits"].reshape(-1), hits.cpu().numpy()), (depth, flags)
+        assert np.array_equal(a["t"].reshape(-1).view(np.uint32), tt.cpu().numpy().view(np.uint32)), (depth, flags)
+        assert np.array_equal(a["rgb"].reshape(-1).view(np.uint32), rgb.cpu().numpy().view(np.uint32)), (depth, flags)
