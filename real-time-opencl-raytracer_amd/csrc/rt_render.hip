@@ -42,12 +42,6 @@
 
 #include "rt_abi.h"
 
-#ifndef RTK_TRI2
-#define RTK_TRI2 0          // 1: a lane in a leaf loads and tests two of its triangles per iteration
-#endif
-#ifndef RTK_T2
-#define RTK_T2 0            // 1: two-level inner records (a node's child boxes + its children's child boxes)
-#endif
 #ifndef RTK_WF_WAVES
 #define RTK_WF_WAVES 7      // waves per SIMD the wavefront kernels are bounded to
 #endif
@@ -68,12 +62,6 @@ constexpr uint32_t kCntEscape = 31u;
 constexpr int kLdsStack = RTK_LDS_STACK;
 constexpr int kGlobalStack = 64 - kLdsStack;         // slots kLdsStack..63
 constexpr uint32_t kBlockPx = 16;                    // a block = 2 x 2 tiles of 8 x 8 pixels
-// Inner record: {child boxes x3, {r0, r1, ..}} = 4 float4 (64 B); RTK_T2 (A/B): + the left
-// and the right child's own child boxes and refs, 11 float4 (176 B):
-//   [0..2] child boxes, [3] {r0, r1, left's r0, left's r1}, [4..6] left's child boxes,
-//   [7..9] right's child boxes, [10] {right's r0, right's r1, 0, 0}
-constexpr uint32_t kInnerF4 = RTK_T2 ? 11u : 4u;
-constexpr uint32_t kInnerBytes = kInnerF4 * 16u;
 
 struct DevScene {
     const float4* __restrict__ wnodes;   // [n_inner][4]
@@ -193,7 +181,7 @@ struct Stack {
 // wave-distinct, [6] wave iterations, [7] mixed iterations; stride 256 (one block's lanes).
 // vmem = false: a record the wave read once through the scalar cache (the traversal's
 // wave-uniform prologue): a lane fetch and a wave-distinct record, but no quad request.
-__device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id, bool vmem = true, bool iter = true) {
+__device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id, bool vmem = true) {
     const uint64_t act = __builtin_amdgcn_read_exec();
     const int lane = (int)(threadIdx.x & 63u);
     bool quad_first = true, wave_first = true;
@@ -209,7 +197,7 @@ __device__ __forceinline__ void fetch_count(uint32_t* fc, bool leaf, uint32_t id
     fc[t * 256] += 1u;
     fc[(2 + t) * 256] += (vmem && quad_first) ? 1u : 0u;
     fc[(4 + t) * 256] += wave_first ? 1u : 0u;
-    if (iter && lane == (int)__builtin_ctzll(act)) {   // (iter false: a second record of the same iteration)
+    if (lane == (int)__builtin_ctzll(act)) {
         fc[6 * 256] += 1u;
         fc[7 * 256] += (lm != 0 && (act & ~lm) != 0) ? 1u : 0u;
     }
@@ -760,7 +748,6 @@ struct rt_ctx {
     struct { bool on = false; unsigned long long* d_counts = nullptr; } trace;   // rt_fetch_counts
     // rt_render's row groups: one stream (so one frame slot) and one "rendered" event per group
     hipStream_t gstream[8] = {};
-    hipEvent_t gdone[8] = {};
     hipEvent_t gstart = nullptr;
     std::vector<FrameSlot*> last_group;   // the slots of the last grouped rt_render
     bool timing_valid = false;
@@ -1106,7 +1093,6 @@ int rt_destroy(rt_ctx* c) {
             if (e) (void)hipEventDestroy(e);
     for (int g = 0; g < 8; ++g) {
         if (c->gstream[g]) (void)hipStreamSynchronize(c->gstream[g]);
-        if (c->gdone[g]) (void)hipEventDestroy(c->gdone[g]);
         if (c->gstream[g]) (void)hipStreamDestroy(c->gstream[g]);
     }
     if (c->gstart) (void)hipEventDestroy(c->gstart);
@@ -1213,13 +1199,13 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
             }
         }
     }
-    std::vector<float4> wn((size_t)std::max(n_inner, 1) * rtk::kInnerF4, make_float4(0, 0, 0, 0));
+    std::vector<float4> wn((size_t)std::max(n_inner, 1) * 4, make_float4(0, 0, 0, 0));
     bool fast_ok = true;  // slab-test fast quotient domain (rt_kernel_body.inc axis_ok)
     for (int32_t n = 0; n < nn; ++n) {
         if (inner_id[n] < 0) continue;
         const rt_bvh_node& L = nodes[nodes[n].offset_left];
         const rt_bvh_node& R = nodes[nodes[n].offset_right];
-        float4* q = &wn[(size_t)inner_id[n] * rtk::kInnerF4];
+        float4* q = &wn[(size_t)inner_id[n] * 4];
         // axis-major: {L.min, R.min, L.max, R.max} per axis (rt_kernel_body.inc slab2_pk)
         q[0] = make_float4(L.min.x, R.min.x, L.max.x, R.max.x);
         q[1] = make_float4(L.min.y, R.min.y, L.max.y, R.max.y);
@@ -1229,24 +1215,6 @@ int rt_upload_scene(rt_ctx* c, const rt_float4* verts, int32_t nv, const int32_t
         std::memcpy(&f0, &r0, 4);
         std::memcpy(&f1, &r1, 4);
         q[3] = make_float4(f0, f1, 0.0f, 0.0f);
-        if (RTK_T2) {   // each inner child's own child boxes and refs (its record's [0..3])
-            for (int side = 0; side < 2; ++side) {
-                const int32_t ch = side ? nodes[n].offset_right : nodes[n].offset_left;
-                if (inner_id[ch] < 0) continue;
-                const rt_bvh_node& cl = nodes[nodes[ch].offset_left];
-                const rt_bvh_node& cr = nodes[nodes[ch].offset_right];
-                float4* g = q + 4 + 3 * side;
-                g[0] = make_float4(cl.min.x, cr.min.x, cl.max.x, cr.max.x);
-                g[1] = make_float4(cl.min.y, cr.min.y, cl.max.y, cr.max.y);
-                g[2] = make_float4(cl.min.z, cr.min.z, cl.max.z, cr.max.z);
-                uint32_t g0 = ref_of[nodes[ch].offset_left], g1 = ref_of[nodes[ch].offset_right];
-                float h0, h1;
-                std::memcpy(&h0, &g0, 4);
-                std::memcpy(&h1, &g1, 4);
-                if (side) q[10] = make_float4(h0, h1, 0.0f, 0.0f);
-                else { q[3].z = h0; q[3].w = h1; }
-            }
-        }
         for (int k = 0; k < 3; ++k) {
             const float* qf = &q[k].x;
             for (int j = 0; j < 4; ++j) {
@@ -1636,29 +1604,22 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     return RT_OK;
 }
 
-// rt_render's overlap of the frame's readback with its rendering (raytrace_gpgpu renders the
-// whole frame, then reads it back: RayTracer.cpp:330-344).  A frame of at least
-// kGroupMinPixels is cut into RTK_RENDER_GROUPS groups of contiguous rows (rt_tiling with one
-// band per "rank", so a group's rows are one contiguous run of the frame and of its aux
-// planes), each rendered straight into its part of the frame buffer on its own stream (its
-// own frame slot and longest-first order); a group's rows go to the host as soon as it is
-// done, while the next groups render.  RTK_RENDER_CHAIN 1: the groups render one after
-// another (each stream waits for the previous group's kernels), so the first rows finish
-// first; 0: concurrently.  The pixels are the same as one whole-frame launch's (a pixel's
-// arithmetic does not depend on how the frame is cut: DESIGN.md 5).
-#ifndef RTK_RENDER_GROUPS
-#define RTK_RENDER_GROUPS 4
-#endif
-#ifndef RTK_RENDER_CHAIN
-#define RTK_RENDER_CHAIN 0
-#endif
-#ifndef RTK_RENDER_PRIO
-#define RTK_RENDER_PRIO 0    // 1: the first group's stream gets the device's highest priority
-#endif
-#ifndef RTK_RENDER_ZC
-#define RTK_RENDER_ZC 0      // 1: pinned, device-mapped host memory is rendered into directly (no readback)
-#endif
-static_assert(RTK_RENDER_GROUPS >= 1 && RTK_RENDER_GROUPS + (RTK_RENDER_CHAIN == 2) <= 8, "rt_render: at most 8 streams");
+// rt_render: the reference's synchronous boundary (raytrace_gpgpu renders the whole frame, then
+// reads it back: RayTracer.cpp:330-344), with the readback overlapped with the rendering.
+//  * Pinned host memory the device can write (hipHostMalloc, or registered as mapped): the
+//    frame is rendered straight into it; the kernel's pixel stores cross the host link while
+//    the frame renders, with no readback after it (C3: 0.40 ms per frame against 0.55 for
+//    render-then-copy, profiles/r04/ab/host_boundary_ab.log).
+//  * Otherwise (pageable memory, or aux planes wanted), a frame of at least kGroupMinPixels is
+//    cut into kRenderGroups groups of contiguous rows (rt_tiling with one band per "rank", so a
+//    group's rows are one contiguous run of the frame and of its aux planes), each rendered
+//    straight into its part of the device frame on its own stream (its own frame slot and
+//    longest-first order), concurrently; a group's rows are copied to the host as soon as it is
+//    done (C3 pageable: 0.49 vs 0.55 ms; 3, 6 or 8 groups, stream priorities, or the groups
+//    rendered one after another on one or several streams measured slower, same log).
+// The pixels are those of one whole-frame launch (a pixel's arithmetic does not depend on how
+// the frame is cut: DESIGN.md 5; tests/test_render_gpu.py test_render_readback_paths_agree).
+constexpr uint32_t kRenderGroups = 4;
 constexpr uint64_t kGroupMinPixels = 512 * 512;
 
 int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr,
@@ -1678,7 +1639,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         if ((rc = ensure(c, c->d_rgb, c->rgb_cap, npix * 3))) return rc;
         dev = rt_aux{c->d_hits, c->d_t, c->d_rgb};
     }
-    if (RTK_RENDER_ZC && !want) {
+    if (!want) {
         // the caller's buffer is pinned host memory the device can write (hipHostMalloc, or
         // registered as mapped): the kernel's pixel stores go straight to it over the host link
         // while the frame renders, with no readback after it
@@ -1692,7 +1653,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         (void)hipGetLastError();   // pageable memory: not an error, the readback path below
     }
     // the group's rows: band_rows a multiple of the 16-row block, at most one band per group
-    uint32_t groups = npix >= kGroupMinPixels ? RTK_RENDER_GROUPS : 1;
+    uint32_t groups = npix >= kGroupMinPixels ? kRenderGroups : 1;
     const uint32_t band_rows = ((h + groups - 1) / groups + 15u) & ~15u;
     groups = (h + band_rows - 1) / band_rows;
     if (groups <= 1) {
@@ -1707,17 +1668,8 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         HIPC(c, hipStreamSynchronize(c->stream));
         return RT_OK;
     }
-    // streams: group g's readback (and, unless RTK_RENDER_CHAIN 2, its kernels) on gstream[g];
-    // RTK_RENDER_CHAIN 2: every group's kernels one after another on gstream[groups]
-    const bool one_render_stream = RTK_RENDER_CHAIN == 2;
-    for (uint32_t g = 0; g < groups + (one_render_stream ? 1u : 0u); ++g) {
-        if (!c->gstream[g]) {
-            int lo = 0, hi = 0;
-            if (RTK_RENDER_PRIO) HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIPC(c, hipStreamCreateWithPriority(&c->gstream[g], hipStreamNonBlocking, g == 0 ? hi : lo));
-        }
-        if (!c->gdone[g]) HIPC(c, hipEventCreateWithFlags(&c->gdone[g], hipEventDisableTiming));
-    }
+    for (uint32_t g = 0; g < groups; ++g)   // group g's kernels and readback on gstream[g]
+        if (!c->gstream[g]) HIPC(c, hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking));
     // after whatever the ctx's own stream still holds (the synchronous entry points leave it idle)
     if (!c->gstart) HIPC(c, hipEventCreateWithFlags(&c->gstart, hipEventDisableTiming));
     HIPC(c, hipEventRecord(c->gstart, c->stream));
@@ -1725,9 +1677,8 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
     // every group's kernels first, then the readbacks in group order: a copy into pageable
     // memory may block the host until it is done, and the later groups must already be queued
     for (uint32_t g = 0; g < groups; ++g) {
-        hipStream_t s = c->gstream[one_render_stream ? groups : g];
-        if (!one_render_stream || g == 0)
-            HIPC(c, hipStreamWaitEvent(s, RTK_RENDER_CHAIN == 1 && g ? c->gdone[g - 1] : c->gstart, 0));
+        hipStream_t s = c->gstream[g];
+        HIPC(c, hipStreamWaitEvent(s, c->gstart, 0));
         const rt_tiling t{(int32_t)g, (int32_t)groups, (int32_t)band_rows, 0};
         const size_t p0 = (size_t)g * band_rows * w;
         rt_aux ga{nullptr, nullptr, nullptr};
@@ -1735,8 +1686,6 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         rc = rt_render_device(c, w, h, depth, flags, &t, c->d_out + p0, want ? &ga : nullptr, s);
         if (rc) return rc;
         slots.push_back(c->last_slot);
-        if (RTK_RENDER_CHAIN) HIPC(c, hipEventRecord(c->gdone[g], s));
-        if (one_render_stream) HIPC(c, hipStreamWaitEvent(c->gstream[g], c->gdone[g], 0));
     }
     for (uint32_t g = 0; g < groups; ++g) {
         hipStream_t s = c->gstream[g];
@@ -1748,7 +1697,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
             if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb + p0 * 3, c->d_rgb + p0 * 3, np * 3 * 4, hipMemcpyDeviceToHost, s));
         }
     }
-    for (uint32_t g = 0; g < groups + (one_render_stream ? 1u : 0u); ++g) HIPC(c, hipStreamSynchronize(c->gstream[g]));
+    for (uint32_t g = 0; g < groups; ++g) HIPC(c, hipStreamSynchronize(c->gstream[g]));
     c->last_group = slots;
     return RT_OK;
 }
