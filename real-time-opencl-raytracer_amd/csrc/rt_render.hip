@@ -137,6 +137,9 @@ struct TQ {
     uint32_t* cursor;       // the launch's work cursor (zeroed per frame)
 };
 constexpr uint32_t kNoRay = 0xFFFFFFFFu;
+#ifndef RTK_REFILL_QUAD
+#define RTK_REFILL_QUAD 1   // refill whole quads with four consecutive rays
+#endif
 #ifndef RTK_REFILL_MIN
 #define RTK_REFILL_MIN 16
 #endif
