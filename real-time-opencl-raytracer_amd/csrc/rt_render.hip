@@ -126,6 +126,33 @@ struct WQ {
 };
 constexpr uint32_t kSegRays = 64;
 
+// Work distribution of the persistent wavefront kernels: a wave takes the next 64-ray group of
+// a queue from one of eight cursors, 128 B apart (its block's group of XCD-sharing blocks,
+// blockIdx % 8; MI355X_MICROARCH.md: blocks b and b + 8 share an XCD); cursor c hands out the
+// groups c, c + 8, c + 16, ..., so all XCDs work through the queue's screen order together, and a
+// wave whose cursor is used up takes from the next one.  One cursor for the whole chip
+// serialises every grab on one address: ~8 ns each, 30 k grabs per C5 bounce launch
+// (profiles/r04: a persistent shading pass over C5's bounce-1 queue took 0.25 ms on one cursor).
+constexpr uint32_t kCursors = 8, kCursorStride = 32;
+constexpr size_t kCursorSet = (size_t)kCursors * kCursorStride;
+constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t grab_group(uint32_t* cursors, uint32_t ngroups, uint32_t& home) {
+    uint32_t g = kNoGroup, h = home;
+    if ((threadIdx.x & 63u) == 0) {
+        for (uint32_t k = 0; k < kCursors; ++k) {
+            const uint32_t c = (h + k) & (kCursors - 1u);
+            const uint32_t gg = c + kCursors * atomicAdd(cursors + c * kCursorStride, 1u);
+            if (gg < ngroups) {
+                g = gg;
+                h = c;
+                break;
+            }
+        }
+    }
+    home = __builtin_amdgcn_readfirstlane(h);
+    return __builtin_amdgcn_readfirstlane(g);
+}
+
 // Split bounces (RTK_SPLIT, rt_kernel_body.inc wf_trace_kernel / wf_shade_kernel / wf_shadow_finish_kernel)
 struct TQ {
     const QRay* q;          // closest: the bounce queue ...
@@ -798,7 +825,10 @@ static std::string g_err;
 
 // frame counters (one parity set): 8 per bounce ([0] queue size, [2] the bounce launch's
 // work cursor), then the restart count (then, sized per frame, the queues' chunk sums)
-constexpr size_t kBounceWords = 8;
+// per bounce k: [0] its queue size, then (128-B aligned) three sets of work cursors of its
+// persistent kernels (rtk::grab_group): the bounce / shade kernel's, and the split bounces'
+// closest-hit and shadow traversals'
+constexpr size_t kBounceWords = 32 + 3 * rtk::kCursorSet;
 constexpr size_t kRestartSlot = kBounceWords * (RT_MAX_DEPTH + 1);
 constexpr size_t kCounters = kRestartSlot + 1;
 
@@ -1514,7 +1544,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const size_t nseg = (size_t)F.num_blocks * 4;   // bounce 0's waves; later queues have fewer groups
     const size_t nchunk = (nseg + rtk::kChunkSegs - 1) / rtk::kChunkSegs;
     const size_t nsuper = (nseg + rtk::kSuperSegs - 1) / rtk::kSuperSegs;
-    const size_t set_words = kCounters + (depth > 1 ? (size_t)(depth - 1) * (nchunk + nsuper) : 0);
+    const size_t set_words = (kCounters + (depth > 1 ? (size_t)(depth - 1) * (nchunk + nsuper) : 0) + 31) & ~(size_t)31;
     if (!L.d_wcnt || L.wcnt_set < set_words) {
         if ((rc = ensure(c, L.d_wcnt, L.wcnt_cap, 2 * set_words))) return rc;
         HIPC(c, hipMemsetAsync(L.d_wcnt, 0, 2 * set_words * sizeof(uint32_t), s));
@@ -1654,19 +1684,19 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.seg_cnt = L.d_seg;
             W.chunk_sum = sums(k + 1);
             W.super_sum = sums(k + 1) + nchunk;
-            W.fetch = bc + 2;
+            W.fetch = bc + 32;
             W.bounce = k;
             if (split) {
                 // closest hits (refilling traversal) -> shading, shadow rays, next rays -> shadow hits
-                // (refilling traversal) -> shadow sums / finished pixels; work cursors bc[2..4]
-                rtk::TQ q1{qbuf(k), L.d_perm, nullptr, nullptr, bc, L.d_hb, bc + 3};
+                // (refilling traversal) -> shadow sums / finished pixels; three cursor sets
+                rtk::TQ q1{qbuf(k), L.d_perm, nullptr, nullptr, bc, L.d_hb, bc + 32 + rtk::kCursorSet};
                 void* a1[] = {&S, &O, &q1};
                 HIPC(c, hipLaunchKernel(kernel_trace(math, true, traced), dim3(c->wf_trace_grid[math]), dim3(256), a1, 0, s));
                 rtk::SB sb{L.d_hb, L.d_sray, L.d_sres, L.d_col, L.d_nslot};
                 void* a2[] = {&S, &Fb, &O, &W, &sb, &ax};
                 HIPC(c, hipLaunchKernel(kernel_shade(math), dim3(c->wf_grid[math]), dim3(256), a2, 0, s));
                 if (!(flags & RT_FLAG_NO_SHADOW)) {
-                    rtk::TQ q2{nullptr, nullptr, L.d_sray, L.d_hb, bc, L.d_sres, bc + 4};
+                    rtk::TQ q2{nullptr, nullptr, L.d_sray, L.d_hb, bc, L.d_sres, bc + 32 + 2 * rtk::kCursorSet};
                     void* a3[] = {&S, &O, &q2};
                     HIPC(c, hipLaunchKernel(kernel_trace(math, false, traced), dim3(c->wf_trace_grid[math]), dim3(256), a3, 0, s));
                     void* a4[] = {&Fb, &O, &W, &sb, &ax};
