@@ -42,9 +42,6 @@
 
 #include "rt_abi.h"
 
-#ifndef RTK_SPLIT
-#define RTK_SPLIT 1          // bounces >= 1 in split phases with refilling traversal (wf_trace_kernel)
-#endif
 #ifndef RTK_WF_WAVES
 #define RTK_WF_WAVES 7      // waves per SIMD the wavefront kernels are bounded to
 #endif
@@ -121,7 +118,7 @@ struct WQ {
     uint32_t* super_sum;      // rays per kSuperSegs segments of `out` (zeroed per frame)
     uint32_t seg;             // the segment this wave appends to (set per wave)
     uint32_t* seg_fill;       // the wave's LDS word: rays appended to `seg` so far
-    uint32_t* fetch;          // the launch's work cursor
+    uint32_t* fetch;          // the launch's work cursors (grab_group)
     int bounce;
 };
 constexpr uint32_t kSegRays = 64;
@@ -132,7 +129,8 @@ constexpr uint32_t kSegRays = 64;
 // groups c, c + 8, c + 16, ..., so all XCDs work through the queue's screen order together, and a
 // wave whose cursor is used up takes from the next one.  One cursor for the whole chip
 // serialises every grab on one address: ~8 ns each, 30 k grabs per C5 bounce launch
-// (profiles/r04: a persistent shading pass over C5's bounce-1 queue took 0.25 ms on one cursor).
+// (C5: 0.904 vs 0.924 ms per frame, profiles/r04/ab/split_cursor_ab.log; a persistent pass that
+// only shaded C5's bounce-1 queue took 0.25 ms on one cursor, 0.16 ms on eight).
 constexpr uint32_t kCursors = 8, kCursorStride = 32;
 constexpr size_t kCursorSet = (size_t)kCursors * kCursorStride;
 constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
@@ -152,35 +150,6 @@ __device__ __forceinline__ uint32_t grab_group(uint32_t* cursors, uint32_t ngrou
     home = __builtin_amdgcn_readfirstlane(h);
     return __builtin_amdgcn_readfirstlane(g);
 }
-
-// Split bounces (RTK_SPLIT, rt_kernel_body.inc wf_trace_kernel / wf_shade_kernel / wf_shadow_finish_kernel)
-struct TQ {
-    const QRay* q;          // closest: the bounce queue ...
-    const uint32_t* perm;   // ... in its dense order
-    const float4* sray;     // any-hit: shadow ray i = {o.xyz, pix} at [2 i], {d.xyz, 0} at [2 i + 1] (ray_init inputs)
-    const int2* gate;       // any-hit: the closest-hit results; hit < 0 = no shadow ray
-    const uint32_t* count;  // rays in the queue
-    int2* res;              // [i] {hit, t bits}
-    uint32_t* cursor;       // the launch's work cursor (zeroed per frame)
-};
-constexpr uint32_t kNoRay = 0xFFFFFFFFu;
-#ifndef RTK_REFILL_QUAD
-#define RTK_REFILL_QUAD 1   // refill whole quads with four consecutive rays
-#endif
-#ifndef RTK_REFILL_MIN
-#define RTK_REFILL_MIN 16
-#endif
-constexpr int kRefillMin = RTK_REFILL_MIN;   // refill once this many lanes are idle (or all of them)
-
-// Per-ray buffers of a split bounce (index = the ray's position i in the queue's dense order).
-struct SB {
-    const int2* hit;        // closest-hit results
-    float4* sray;           // shadow rays (wf_trace_kernel<false> input)
-    const int2* shadow;     // shadow results
-    float4* col;            // colour so far (+ rez) and shadow sum before this bounce's shadow ray
-    uint32_t* nslot;        // the next queue's slot of the ray's continuation, or kNoRay
-};
-
 
 struct Outputs {
     uint32_t* out;
@@ -791,12 +760,6 @@ struct rt_ctx {
         size_t wcnt_set = 0;                                                //   of this many words each
         uint32_t* d_perm = nullptr; size_t perm_cap = 0;                    // wavefront: dense queue order
         uint32_t* d_seg = nullptr; size_t seg_cap = 0;                      // wavefront: rays per queue segment
-        // split bounces (RTK_SPLIT): per dense ray, closest / shadow results, shadow ray, colour, continuation slot
-        int2* d_hb = nullptr; size_t hb_cap = 0;
-        int2* d_sres = nullptr; size_t sres_cap = 0;
-        float4* d_sray = nullptr; size_t sray_cap = 0;
-        float4* d_col = nullptr; size_t col_cap = 0;
-        uint32_t* d_nslot = nullptr; size_t nslot_cap = 0;
         uint32_t* d_cost = nullptr; size_t cost_cap = 0;   // adaptive order: per-tile times,
         uint32_t* d_lpt = nullptr; size_t lpt_cap = 0;     //   the longest-first order built from them,
         uint32_t* d_done = nullptr;                        //   and the finished-block counter
@@ -810,8 +773,6 @@ struct rt_ctx {
     uint32_t order_tx = 0, order_ty = 0;
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
-    int wf_trace_grid[3] = {0, 0, 0};   // ... of the split bounces' traversal kernel
-    int cus = 0;
     struct { bool on = false; unsigned long long* d_counts = nullptr; } trace;   // rt_fetch_counts
     // rt_render's row groups: one stream (so one frame slot) and one "rendered" event per group
     hipStream_t gstream[8] = {};
@@ -825,10 +786,9 @@ static std::string g_err;
 
 // frame counters (one parity set): 8 per bounce ([0] queue size, [2] the bounce launch's
 // work cursor), then the restart count (then, sized per frame, the queues' chunk sums)
-// per bounce k: [0] its queue size, then (128-B aligned) three sets of work cursors of its
-// persistent kernels (rtk::grab_group): the bounce / shade kernel's, and the split bounces'
-// closest-hit and shadow traversals'
-constexpr size_t kBounceWords = 32 + 3 * rtk::kCursorSet;
+// per bounce k: [0] its queue size, then (128-B aligned) the work cursors of its persistent
+// bounce kernel (rtk::grab_group)
+constexpr size_t kBounceWords = 32 + rtk::kCursorSet;
 constexpr size_t kRestartSlot = kBounceWords * (RT_MAX_DEPTH + 1);
 constexpr size_t kCounters = kRestartSlot + 1;
 
@@ -856,8 +816,7 @@ static int ensure(rt_ctx* c, T*& p, size_t& cap, size_t n) {
 
 static void free_slot(rt_ctx::FrameSlot& f) {
     for (void* p : {(void*)f.d_gstack, (void*)f.d_wq[0], (void*)f.d_wq[1], (void*)f.d_wcnt,
-                    (void*)f.d_perm, (void*)f.d_seg, (void*)f.d_cost, (void*)f.d_lpt, (void*)f.d_done,
-                    (void*)f.d_hb, (void*)f.d_sres, (void*)f.d_sray, (void*)f.d_col, (void*)f.d_nslot})
+                    (void*)f.d_perm, (void*)f.d_seg, (void*)f.d_cost, (void*)f.d_lpt, (void*)f.d_done})
         if (p) (void)hipFree(p);
     if (f.idle) (void)hipEventDestroy(f.idle);
     f = rt_ctx::FrameSlot{};
@@ -980,12 +939,6 @@ template <int M> struct Kernels;
             return next ? (void*)NS::first_bounce_kernel<true, true, true> : (void*)NS::first_bounce_kernel<true, false, true>; \
         }                                                                                                  \
         static void* traced_bounce() { return (void*)NS::wf_bounce_kernel<true, true>; }                  \
-        static void* trace(bool closest, bool tr) {                                                        \
-            return closest ? (tr ? (void*)NS::wf_trace_kernel<true, true> : (void*)NS::wf_trace_kernel<true, false>) \
-                           : (tr ? (void*)NS::wf_trace_kernel<false, true> : (void*)NS::wf_trace_kernel<false, false>); \
-        }                                                                                                  \
-        static void* shade() { return (void*)NS::wf_shade_kernel; }                                        \
-        static void* shadow_finish() { return (void*)NS::wf_shadow_finish_kernel; }                        \
     };
 RTK_KERNELS(0, rtk_strict)
 RTK_KERNELS(1, rtk_hw)
@@ -1003,13 +956,6 @@ static void* kernel_traced(int m, bool next) {
 }
 static void* kernel_traced_bounce(int m) {
     return m == 0 ? Kernels<0>::traced_bounce() : m == 1 ? Kernels<1>::traced_bounce() : Kernels<2>::traced_bounce();
-}
-static void* kernel_trace(int m, bool closest, bool tr) {
-    return m == 0 ? Kernels<0>::trace(closest, tr) : m == 1 ? Kernels<1>::trace(closest, tr) : Kernels<2>::trace(closest, tr);
-}
-static void* kernel_shade(int m) { return m == 0 ? Kernels<0>::shade() : m == 1 ? Kernels<1>::shade() : Kernels<2>::shade(); }
-static void* kernel_shadow_finish(int m) {
-    return m == 0 ? Kernels<0>::shadow_finish() : m == 1 ? Kernels<1>::shadow_finish() : Kernels<2>::shadow_finish();
 }
 static void* kernel_bounce(int m, bool fast) {
     return m == 0 ? Kernels<0>::bounce(fast) : m == 1 ? Kernels<1>::bounce(fast) : Kernels<2>::bounce(fast);
@@ -1618,27 +1564,15 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
             HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (const void*)kernel_bounce(math, true), 256, 0));
             c->wf_grid[math] = std::max(8, std::max(b1, 1) * cus);
-            HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (const void*)kernel_trace(math, true, false), 256, 0));
-            c->wf_trace_grid[math] = std::max(8, std::max(b1, 1) * cus);
-            c->cus = cus;
         }
         // segmented queues: bounce 0's waves (4 per block) each own a segment of 64 slots;
         // later bounces have at most as many 64-ray groups
         const size_t slots = nseg * rtk::kSegRays;
-        // split bounces: the fast kernels with the packed quotient (otherwise the fused bounce kernel)
-        const bool split = RTK_SPLIT && depth > 1 && fast && S.fast_div;
         if (depth > 1) {
             if ((rc = ensure(c, L.d_wq[0], L.wq_cap[0], slots * 3))) return rc;   // 3 float4 per QRay
             if ((rc = ensure(c, L.d_wq[1], L.wq_cap[1], slots * 3))) return rc;
             if ((rc = ensure(c, L.d_perm, L.perm_cap, slots))) return rc;
             if ((rc = ensure(c, L.d_seg, L.seg_cap, nseg))) return rc;
-        }
-        if (split) {
-            if ((rc = ensure(c, L.d_hb, L.hb_cap, slots))) return rc;
-            if ((rc = ensure(c, L.d_sres, L.sres_cap, slots))) return rc;
-            if ((rc = ensure(c, L.d_sray, L.sray_cap, slots * 2))) return rc;
-            if ((rc = ensure(c, L.d_col, L.col_cap, slots))) return rc;
-            if ((rc = ensure(c, L.d_nslot, L.nslot_cap, slots))) return rc;
         }
         const bool sort = (flags & RT_FLAG_WF_SORT) && depth > 1;
         // the local sort's key axis: the scene box's thinnest
@@ -1686,24 +1620,6 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.super_sum = sums(k + 1) + nchunk;
             W.fetch = bc + 32;
             W.bounce = k;
-            if (split) {
-                // closest hits (refilling traversal) -> shading, shadow rays, next rays -> shadow hits
-                // (refilling traversal) -> shadow sums / finished pixels; three cursor sets
-                rtk::TQ q1{qbuf(k), L.d_perm, nullptr, nullptr, bc, L.d_hb, bc + 32 + rtk::kCursorSet};
-                void* a1[] = {&S, &O, &q1};
-                HIPC(c, hipLaunchKernel(kernel_trace(math, true, traced), dim3(c->wf_trace_grid[math]), dim3(256), a1, 0, s));
-                rtk::SB sb{L.d_hb, L.d_sray, L.d_sres, L.d_col, L.d_nslot};
-                void* a2[] = {&S, &Fb, &O, &W, &sb, &ax};
-                HIPC(c, hipLaunchKernel(kernel_shade(math), dim3(c->wf_grid[math]), dim3(256), a2, 0, s));
-                if (!(flags & RT_FLAG_NO_SHADOW)) {
-                    rtk::TQ q2{nullptr, nullptr, L.d_sray, L.d_hb, bc, L.d_sres, bc + 32 + 2 * rtk::kCursorSet};
-                    void* a3[] = {&S, &O, &q2};
-                    HIPC(c, hipLaunchKernel(kernel_trace(math, false, traced), dim3(c->wf_trace_grid[math]), dim3(256), a3, 0, s));
-                    void* a4[] = {&Fb, &O, &W, &sb, &ax};
-                    HIPC(c, hipLaunchKernel(kernel_shadow_finish(math), dim3((uint32_t)c->cus * 4u), dim3(256), a4, 0, s));
-                }
-                continue;
-            }
             void* args[] = {&S, &Fb, &O, &W, &ax};
             HIPC(c, hipLaunchKernel(traced ? kernel_traced_bounce(math) : kernel_bounce(math, fast), dim3(c->wf_grid[math]),
                                     dim3(256), args, 0, s));
