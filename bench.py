@@ -765,6 +765,23 @@ def run(args, world, result_out=None):
     # (untimed for `value`) the reference's own boundary: rt_render, synchronous, the frame
     # read back into host memory (raytrace_gpgpu: launch + clFinish + clEnqueueReadBuffer,
     # RayTracer.cpp:330-344); pageable numpy and pinned host buffers
+    # (untimed for `value`) one frame in flight: each frame's kernels from launch to completion,
+    # nothing overlapping it -- the frame's critical path, which the frames in flight of the
+    # timed region hide (C2: 0.25 ms alone against 0.08 ms per frame with four in flight)
+    frame_latency = None
+    if world == 1 and not args.shard:
+        lat = []
+        for _ in range(21):
+            t1 = time.perf_counter()
+            launch(out_ptr[0][0], sh[0])
+            torch.cuda.synchronize(dev)
+            lat.append((time.perf_counter() - t1) * 1e3)
+        lat = sorted(lat[1:])
+        frame_latency = {"ms_per_frame_median": round(lat[len(lat) // 2], 4), "ms_per_frame_min": round(lat[0], 4),
+                         "frames": len(lat), "how": "one frame at a time: launch + device synchronize, host clock"}
+        if orbit_params is not None:
+            set_params(hdl, orbit_params[0])
+
     host_boundary = None
     if world == 1 and not args.shard:
         def host_rate(buf_ptr, n=20):
@@ -1041,6 +1058,8 @@ def run(args, world, result_out=None):
             "refilled only after rank 0 has presented (and consumed) its previous frame"))
     if host_boundary is not None:
         res["config"]["host_boundary"] = host_boundary
+    if frame_latency is not None:
+        res["config"]["frame_latency"] = frame_latency
     print(json.dumps(res), file=result_out or sys.stdout, flush=True)
     if use_dist:
         dist.barrier()
