@@ -91,12 +91,11 @@ def main():
         d = occ["derived"]
         res["occupancy"] = {
             "waves_per_simd": round(d["waves_per_simd"], 3) if "waves_per_simd" in d else None,
-            "waves_per_simd_active_cu": round(d["waves_per_simd_active_cu"], 3) if "waves_per_simd_active_cu" in d else None,
             "max_waves_per_simd": 8,
             "kernel": occ["kernel"],
-            "source": "rocprofv3 --pmc MeanOccupancyPerCU / MeanOccupancyPerActiveCU (SQ_LEVEL_WAVES accumulated over "
-                      "GRBM_GUI_ACTIVE per CU, rocprofiler-sdk counter_defs.yaml for gfx950) / 4 SIMDs, one frame in "
-                      "flight (scripts/pmc_configs.sh)"}
+            "source": "rocprofv3 --pmc MeanOccupancyPerCU (SQ_LEVEL_WAVES accumulated over GRBM_GUI_ACTIVE per CU, "
+                      "rocprofiler-sdk counter_defs.yaml for gfx950) / 4 SIMDs; counters are collected per dispatch, "
+                      "so this is one frame's kernel alone, ramp-up and tail included (scripts/pmc_configs.sh)"}
     json.dump(res, open(os.path.join(out, f"pmc_{cfg}.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
