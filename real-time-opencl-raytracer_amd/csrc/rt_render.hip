@@ -42,6 +42,9 @@
 
 #include "rt_abi.h"
 
+#ifndef RTK_SORT_QUADS
+#define RTK_SORT_QUADS 0     // 1: the bounce sort keeps aligned groups of four slots together
+#endif
 #ifndef RTK_WF_WAVES
 #define RTK_WF_WAVES 7      // waves per SIMD the wavefront kernels are bounded to
 #endif
@@ -428,6 +431,11 @@ __global__ void __launch_bounds__(256) wf_compact_sort_kernel(const QRay* __rest
             const float d = axis == 0 ? b.x : axis == 1 ? b.y : b.z;
             k = d == d ? (uint32_t)min(max((int)((d + 1.0f) * 4.0f), 0), 7) : 0u;
         }
+#if RTK_SORT_QUADS
+        // four consecutive slots (a quad of neighbouring pixels, appended side by side) keep the key
+        // of their first: they stay together, in one quad of lanes of the bounce kernel
+        k = (uint32_t)__shfl((int)k, (int)(lane & ~3u));
+#endif
         uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
         for (int bit = 0; bit < 3; ++bit) {
