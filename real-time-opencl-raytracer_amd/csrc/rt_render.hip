@@ -42,12 +42,6 @@
 
 #include "rt_abi.h"
 
-#ifndef RTK_LPT_LAG
-#define RTK_LPT_LAG 0       // 1: a frame's last block orders the next frame by the previous frame's block times
-#endif
-#ifndef RTK_SORT_QUADS
-#define RTK_SORT_QUADS 0     // 1: the bounce sort keeps aligned groups of four slots together
-#endif
 #ifndef RTK_WF_WAVES
 #define RTK_WF_WAVES 7      // waves per SIMD the wavefront kernels are bounded to
 #endif
@@ -96,7 +90,6 @@ struct Frame {
     uint32_t tiles_x, tiles_y, num_blocks;   // blocks of kBlockPx x kBlockPx pixels
     const uint32_t* tile_order;   // [num_blocks] block -> tile (static column strips, or longest-first)
     uint32_t* tile_cost;          // [num_blocks] per-tile time of this frame (adaptive order), or null
-    const uint32_t* cost_sorted;  // the per-tile times the frame's last block sorts (RTK_LPT_LAG: the previous frame's)
     uint32_t* lpt_next;           // [num_blocks] longest-first order for the next frame on this slot
     uint32_t* done;               // blocks finished so far (the last one builds lpt_next)
     uint32_t* zero_next;          // the other parity's frame counters, zeroed by this frame
@@ -335,14 +328,8 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
     __syncthreads();
     if (tid == 0) {
         const uint32_t c = max(max(scratch[0], scratch[1]), max(scratch[2], scratch[3]));
-#if RTK_LPT_LAG
-        // the last block sorts the PREVIOUS frame's times (complete and written back at that
-        // frame's end), so this store need not be waited for: one round trip less per block
-        F.tile_cost[tb] = c;
-#else
         __hip_atomic_store(F.tile_cost + tb, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         const uint32_t prev = __hip_atomic_fetch_add(F.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         scratch[4] = prev + 1u == F.num_blocks ? 1u : 0u;
     }
@@ -355,7 +342,7 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
     hist[tid] = 0;
     __syncthreads();
     for (uint32_t i = tid; i < nb; i += 256)
-        atomicAdd(&hist[lpt_key(__hip_atomic_load(F.cost_sorted + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))], 1u);
+        atomicAdd(&hist[lpt_key(__hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))], 1u);
     __syncthreads();
     // exclusive prefix over the buckets, largest key first (Hillis-Steele on 256 lanes)
     scan[tid] = hist[255 - tid];
@@ -369,7 +356,7 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
     hist[255 - tid] = scan[src * 256 + tid] - hist[255 - tid];   // inclusive -> exclusive
     __syncthreads();
     for (uint32_t i = tid; i < nb; i += 256) {
-        const uint32_t c = __hip_atomic_load(F.cost_sorted + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t c = __hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         F.lpt_next[atomicAdd(&hist[lpt_key(c)], 1u)] = i;
     }
     if (tid == 0) __hip_atomic_store(F.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -441,11 +428,6 @@ __global__ void __launch_bounds__(256) wf_compact_sort_kernel(const QRay* __rest
             const float d = axis == 0 ? b.x : axis == 1 ? b.y : b.z;
             k = d == d ? (uint32_t)min(max((int)((d + 1.0f) * 4.0f), 0), 7) : 0u;
         }
-#if RTK_SORT_QUADS
-        // four consecutive slots (a quad of neighbouring pixels, appended side by side) keep the key
-        // of their first: they stay together, in one quad of lanes of the bounce kernel
-        k = (uint32_t)__shfl((int)k, (int)(lane & ~3u));
-#endif
         uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
         for (int bit = 0; bit < 3; ++bit) {
@@ -1536,13 +1518,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     // Adaptive longest-first order from the previous frame of the same geometry on this
     // slot, built by that frame's last block; the first frame runs the static order.
     F.tile_cost = nullptr;
-    F.cost_sorted = nullptr;
     F.lpt_next = nullptr;
     F.done = nullptr;
     if (!(flags & RT_FLAG_STATIC_ORDER)) {
         const uint32_t units = F.num_blocks;
-        const bool fresh = L.cost_cap < 2 * (size_t)units || !L.d_done;
-        if ((rc = ensure(c, L.d_cost, L.cost_cap, 2 * (size_t)units))) return rc;   // two frames' times (RTK_LPT_LAG)
+        const bool fresh = L.cost_cap < units || !L.d_done;
+        if ((rc = ensure(c, L.d_cost, L.cost_cap, units))) return rc;
         if ((rc = ensure(c, L.d_lpt, L.lpt_cap, units))) return rc;
         if (!L.d_done) {
             size_t one = 0;
@@ -1556,9 +1537,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             L.cost_ready = false;
         }
         if (L.cost_ready) F.tile_order = L.d_lpt;
-        const size_t cp = RTK_LPT_LAG ? (size_t)(L.nframe & 1u) * units : 0;
-        F.tile_cost = L.d_cost + cp;
-        F.cost_sorted = RTK_LPT_LAG ? L.d_cost + (units - cp) : F.tile_cost;
+        F.tile_cost = L.d_cost;
         F.lpt_next = L.d_lpt;
         F.done = L.d_done;
     }
