@@ -774,7 +774,7 @@ struct rt_ctx {
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
     struct { bool on = false; unsigned long long* d_counts = nullptr; } trace;   // rt_fetch_counts
-    // rt_render's row groups: one stream (so one frame slot) and one "rendered" event per group
+    // rt_render's row groups: one stream (so one frame slot) per group, and the event they start after
     hipStream_t gstream[8] = {};
     hipEvent_t gstart = nullptr;
     std::vector<FrameSlot*> last_group;   // the slots of the last grouped rt_render
