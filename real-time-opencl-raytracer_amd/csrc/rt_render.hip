@@ -107,7 +107,10 @@ struct QRay {
 // The producer also adds each count to its chunk's (16 segments) and super-chunk's (1024
 // segments) sum, from which wf_compact_sort_kernel's blocks find where their chunk starts
 // in the bounce's dense order `perm` (compacted, optionally sorted), with no scan launch.
-constexpr uint32_t kChunkSegs = 16, kSuperSegs = 1024;
+#ifndef RTK_CHUNK_SEGS
+#define RTK_CHUNK_SEGS 16
+#endif
+constexpr uint32_t kChunkSegs = RTK_CHUNK_SEGS, kSuperSegs = 1024;
 struct WQ {
     const QRay* in;           // this bounce's rays (segmented)
     const uint32_t* in_count; // rays in it
