@@ -104,11 +104,11 @@ struct QRay {
 // appended, packed from its first slot; seg_cnt[s] says how many.  The producer's wave of
 // segment s is a screen tile's 8x8 pixels (bounce 0) or the 64-ray group s of the previous
 // bounce's order, so the segments are in screen order and no append contends for a counter.
-// The producer also adds each count to its chunk's (16 segments) and super-chunk's (1024
+// The producer also adds each count to its chunk's (kChunkSegs segments) and super-chunk's (1024
 // segments) sum, from which wf_compact_sort_kernel's blocks find where their chunk starts
 // in the bounce's dense order `perm` (compacted, optionally sorted), with no scan launch.
 #ifndef RTK_CHUNK_SEGS
-#define RTK_CHUNK_SEGS 16
+#define RTK_CHUNK_SEGS 32   // segments per sort chunk (C5: 16 -> 0.900 ms, 32 -> 0.881, 64 -> 0.900; profiles/r04/ab/sort_chunk_ab.log)
 #endif
 constexpr uint32_t kChunkSegs = RTK_CHUNK_SEGS, kSuperSegs = 1024;
 struct WQ {
@@ -367,8 +367,8 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
 
 // ---- math-independent kernels ----
 
-// Dense order of a segmented queue (wf_compact_sort_kernel): block b takes the 16 segments
-// [16 b, 16 b + 16), i.e. 1024 slots of one screen-local region (4 tiles of 16x16 pixels at
+// Dense order of a segmented queue (wf_compact_sort_kernel): block b takes the kChunkSegs (32)
+// segments [32 b, 32 b + 32), i.e. 2048 slots of one screen-local region (8 tiles of 16x16 pixels at
 // bounce 1), finds where its rays start in the dense order from the super-chunk and chunk
 // sums before it (d0), and writes perm[d0 ..] with their slots, in slot order -- or with
 // `sort` (RT_FLAG_WF_SORT), stably by the

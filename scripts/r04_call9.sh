@@ -1,0 +1,7 @@
+#!/bin/bash
+# Round 4, call 9: the GPU suite on 32-segment sort chunks, and the A/B against 16 on C5.
+cd ${GRAFT_REPO_ROOT:-.}
+mkdir -p gpurun_out/r04
+scripts/gpu_steps.sh \
+ "pytest_gpu|420|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" \
+ "ab_chunk2|500|scripts/ab_bench.sh 'main ch16' 'c5 c5u' 2"
