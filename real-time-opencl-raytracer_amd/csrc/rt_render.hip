@@ -107,6 +107,9 @@ struct QRay {
 // The producer also adds each count to its chunk's (kChunkSegs segments) and super-chunk's (1024
 // segments) sum, from which wf_compact_sort_kernel's blocks find where their chunk starts
 // in the bounce's dense order `perm` (compacted, optionally sorted), with no scan launch.
+#ifndef RTK_SORT_SCALE
+#define RTK_SORT_SCALE 4    // bounce sort: 2 x this many direction buckets over [-1, 1] (at most 8)
+#endif
 #ifndef RTK_CHUNK_SEGS
 #define RTK_CHUNK_SEGS 32   // segments per sort chunk (C5: 16 -> 0.900 ms, 32 -> 0.881, 64 -> 0.900; profiles/r04/ab/sort_chunk_ab.log)
 #endif
@@ -429,7 +432,7 @@ __global__ void __launch_bounds__(256) wf_compact_sort_kernel(const QRay* __rest
         if (valid && sort) {
             const float4 b = q[j].b;   // {d.xyz, shadow sum}
             const float d = axis == 0 ? b.x : axis == 1 ? b.y : b.z;
-            k = d == d ? (uint32_t)min(max((int)((d + 1.0f) * 4.0f), 0), 7) : 0u;
+            k = d == d ? (uint32_t)min(max((int)((d + 1.0f) * (float)RTK_SORT_SCALE), 0), 2 * RTK_SORT_SCALE - 1) : 0u;
         }
         uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
