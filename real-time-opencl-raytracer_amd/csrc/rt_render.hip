@@ -107,9 +107,6 @@ struct QRay {
 // The producer also adds each count to its chunk's (kChunkSegs segments) and super-chunk's (1024
 // segments) sum, from which wf_compact_sort_kernel's blocks find where their chunk starts
 // in the bounce's dense order `perm` (compacted, optionally sorted), with no scan launch.
-#ifndef RTK_SEG_BAND
-#define RTK_SEG_BAND 1      // first-bounce queue order: tiles in bands of this many tile rows (see seg_rank)
-#endif
 #ifndef RTK_SORT_SCALE
 #define RTK_SORT_SCALE 4    // bounce sort: 2 x this many direction buckets over [-1, 1] (at most 8)
 #endif
@@ -258,18 +255,6 @@ __device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
 }
 
 __device__ __forceinline__ uint32_t block_tile(const Frame& F) { return F.tile_order[blockIdx.x]; }
-
-// The position of tile tb (16x16 pixels, row-major) in the first bounce's queue order: tiles in
-// bands of RTK_SEG_BAND tile rows, column by column inside a band, so a sort chunk of
-// kChunkSegs / 4 consecutive tiles covers a squarer screen region (1: row-major).  A bijection
-// on the tile grid (a last, short band goes column by column over its rows).
-__device__ __forceinline__ uint32_t seg_rank(const Frame& F, uint32_t tb) {
-    if (RTK_SEG_BAND <= 1) return tb;
-    const uint32_t tx = tb % F.tiles_x, ty = tb / F.tiles_x;
-    const uint32_t band = ty / RTK_SEG_BAND, row = ty % RTK_SEG_BAND;
-    const uint32_t rows = min((uint32_t)RTK_SEG_BAND, F.tiles_y - band * RTK_SEG_BAND);
-    return band * RTK_SEG_BAND * F.tiles_x + tx * rows + row;
-}
 
 // Lane -> pixel inside a block's 16x16 pixels: wave w holds 8x8 tile (w % 2, w / 2), lanes
 // in Morton order.  The vector-memory path merges the requests of the four lanes of a quad
