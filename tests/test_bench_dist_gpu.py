@@ -31,7 +31,7 @@ def test_bench_dist_path_assembles_the_frame(i, extra):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist", "--config", "c2", "--direct", "--steps", "4",
            "--warmup", "2", "--no-cpu-baseline", "--cpu-seconds", "0.5"] + extra
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.returncode == 0, _why(p)
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
     assert res["config"]["gathered_frame_equals_single_rank_render"] is True
@@ -47,16 +47,19 @@ def test_bench_dist_shard_diagnostic_completes(gather):
            "--config", "c2", "--direct", "--steps", "8", "--warmup", "2", "--warmup-seconds", "0",
            "--no-cpu-baseline", "--sync-timeout-ms", "2000", "--hang-timeout", "100"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.returncode == 0, _why(p)
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["value"] > 0 and "shard 0/8" in res["config"]["parallelism"]
 
 
 def _why(p):
-    """The part of a failed run's stderr that says why: from its last traceback, else the tail."""
+    """The part of a failed run's stderr that says why: bench.py's own messages (its SystemExit
+    lines and rank notes), the first traceback (a rank's, before the launcher's), and the tail."""
     err = p.stderr
-    i = err.rfind("Traceback (most recent call last)")
-    return err[i:i + 3000] if i >= 0 else err[-3000:]
+    own = [ln for ln in err.splitlines() if "bench.py:" in ln or ln.startswith("rank ")]
+    i = err.find("Traceback (most recent call last)")
+    tb = err[i:i + 2500] if i >= 0 else ""
+    return "\n".join(own[-20:]) + "\n--- first traceback ---\n" + tb + "\n--- tail ---\n" + err[-1500:]
 
 
 def _ranks_on_one_gpu(n, extra, timeout=115):
@@ -74,7 +77,7 @@ def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
     (rt_frame_present), checksums it right then, and every checksum and every frame it holds at
     the end equal its own one-rank render of that frame's camera."""
     p = _ranks_on_one_gpu(n, ["--steps", "24", "--orbit", "0.01", "--frame-check", "every"])
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.returncode == 0, _why(p)
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
     assert res["n_gpus"] == n
@@ -91,7 +94,7 @@ def test_frame_check_catches_a_band_from_another_frame():
     (orbiting camera: every frame differs) must flag exactly that frame."""
     p = _ranks_on_one_gpu(2, ["--steps", "10", "--orbit", "0.01", "--frame-check", "every",
                               "--inject-fault", "wrong-bands"])
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.returncode == 0, _why(p)
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["config"]["frame_check"]["checksum_mismatches"] == 1
     assert res["config"]["gathered_frame_equals_single_rank_render"] is False
@@ -111,7 +114,7 @@ def test_failed_warmup_exchange_falls_back_to_the_rccl_gather():
     which then assemble correctly; the JSON names the fallback."""
     p = _ranks_on_one_gpu(2, ["--steps", "6", "--warmup", "4", "--sync-timeout-ms", "300", "--orbit", "0.01",
                               "--inject-fault", "drop-put-warmup"])
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.returncode == 0, _why(p)
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert "warm-up frame delivery" in res["config"]["band_exchange_fallback"]
     assert "torch.distributed gather" in res["config"]["band_exchange"]
