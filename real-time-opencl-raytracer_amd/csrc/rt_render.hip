@@ -107,12 +107,6 @@ struct QRay {
 // The producer also adds each count to its chunk's (kChunkSegs segments) and super-chunk's (1024
 // segments) sum, from which wf_compact_sort_kernel's blocks find where their chunk starts
 // in the bounce's dense order `perm` (compacted, optionally sorted), with no scan launch.
-#ifndef RTK_SEL_NEXT
-#define RTK_SEL_NEXT 0      // 1: the depth > 1 first-bounce kernel selects record offsets too (SEL)
-#endif
-#ifndef RTK_SEL_BOUNCE
-#define RTK_SEL_BOUNCE 0    // 1: so does the bounce kernel
-#endif
 #ifndef RTK_SORT_SCALE
 #define RTK_SORT_SCALE 4    // bounce sort: 2 x this many direction buckets over [-1, 1] (at most 8)
 #endif
