@@ -639,7 +639,12 @@ def run(args, world, result_out=None):
     # GPU's clocks ramp up over a fraction of a second after the idle scene setup: 20 frames
     # measured right after 5 warm-up frames ran 10 % slower than in steady state).  Every rank
     # warms up as many frames as the slowest-to-warm rank (agreed through an all-reduce, so the
-    # ranks' frame sequences stay in step).
+    # ranks' frame sequences stay in step).  The ranks start it together: rank 0's present of the
+    # first frame waits (bounded by --sync-timeout-ms) for every rank's first put, so a rank still
+    # finishing its set-up must not eat into that bound.
+    torch.cuda.synchronize(dev)
+    if use_dist:
+        dist.barrier()
     for _ in range(args.warmup):
         step()
     drain()

@@ -67,7 +67,7 @@ def _ranks_on_one_gpu(n, extra, timeout=115):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--gather", "ipc", "--pg", "gloo",
            "--config", "c2", "--direct", "--warmup", "2", "--warmup-seconds", "0", "--no-cpu-baseline",
-           "--cpu-seconds", "0.5", "--hang-timeout", "100"] + extra
+           "--cpu-seconds", "0.5", "--hang-timeout", "100", "--sync-timeout-ms", "30000"] + extra
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
 
