@@ -45,6 +45,12 @@
 #ifndef RTK_WF_WAVES
 #define RTK_WF_WAVES 7      // waves per SIMD the wavefront kernels are bounded to
 #endif
+#ifndef RTK_WFB_REF_WAVES
+#define RTK_WFB_REF_WAVES 8 // waves per SIMD the S_ref bounce kernel is bounded to
+#endif
+#ifndef RTK_WF_GRID_PCT
+#define RTK_WF_GRID_PCT 100 // persistent bounce grid, percent of the blocks the chip holds at once
+#endif
 #ifndef RTK_FB_WAVES
 #define RTK_FB_WAVES 8      // waves per SIMD the S_ref depth-1 kernel is bounded to
 #endif
@@ -1569,7 +1575,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             int cus = 0, b1 = 0;
             HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
             HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, (const void*)kernel_bounce(math, true), 256, 0));
-            c->wf_grid[math] = std::max(8, std::max(b1, 1) * cus);
+            c->wf_grid[math] = std::max(8, std::max(b1, 1) * cus * RTK_WF_GRID_PCT / 100);
         }
         // segmented queues: bounce 0's waves (4 per block) each own a segment of 64 slots;
         // later bounces have at most as many 64-ray groups
