@@ -45,6 +45,9 @@
 #ifndef RTK_WF_WAVES
 #define RTK_WF_WAVES 7      // waves per SIMD the wavefront kernels are bounded to
 #endif
+#ifndef RTK_FBN_REF_WAVES
+#define RTK_FBN_REF_WAVES 8 // waves per SIMD the S_ref depth > 1 first-bounce kernel is bounded to
+#endif
 #ifndef RTK_WFB_REF_WAVES
 #define RTK_WFB_REF_WAVES 8 // waves per SIMD the S_ref bounce kernel is bounded to
 #endif
