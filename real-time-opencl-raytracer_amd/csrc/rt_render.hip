@@ -48,6 +48,9 @@
 #ifndef RTK_FBN_REF_WAVES
 #define RTK_FBN_REF_WAVES 8 // waves per SIMD the S_ref depth > 1 first-bounce kernel is bounded to
 #endif
+#ifndef RTK_SEL_NEXT
+#define RTK_SEL_NEXT 0      // offset select (SEL) in the depth > 1 first-bounce kernel too
+#endif
 #ifndef RTK_WFB_REF_WAVES
 #define RTK_WFB_REF_WAVES 8 // waves per SIMD the S_ref bounce kernel is bounded to
 #endif
