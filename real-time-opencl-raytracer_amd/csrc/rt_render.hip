@@ -55,7 +55,8 @@
 #define RTK_WFB_REF_WAVES 8 // waves per SIMD the S_ref bounce kernel is bounded to
 #endif
 #ifndef RTK_WF_GRID_PCT
-#define RTK_WF_GRID_PCT 100 // persistent bounce grid, percent of the blocks the chip holds at once
+#define RTK_WF_GRID_PCT 75  // persistent bounce grid, percent of the blocks the chip holds at once
+                            // (C5 0.838 vs 0.849 ms at 100 %, profiles/r04/ab/grid_8waves_ab.log)
 #endif
 #ifndef RTK_FB_WAVES
 #define RTK_FB_WAVES 8      // waves per SIMD the S_ref depth-1 kernel is bounded to
