@@ -91,14 +91,21 @@ def parse_args(argv=None):
     ap.add_argument("--sync-timeout-ms", type=int, default=10000,
                     help="ipc exchange: bound on a put's wait for its frame set and on rank 0's wait for a frame")
     ap.add_argument("--inject-fault", default="none",
-                    choices=["none", "wrong-bands", "drop-put", "drop-put-warmup", "no-peer", "open-fails"],
+                    choices=["none", "wrong-bands", "drop-put", "drop-put-warmup", "no-peer", "open-fails",
+                             "slow-setup"],
                     help="test only (ipc exchange, N > 1): the last rank puts frame 4's bands from another frame's "
                          "buffer (wrong-bands: the frame check must fail), or skips its put of frame 4 (drop-put: "
                          "frame delivery must fail by timeout), or of frame 1, a warm-up frame (drop-put-warmup: "
                          "the warm-up check must move every rank to the torch.distributed gather); or, at set-up, "
                          "its peer-access check says no (no-peer) or it maps rank 0's frames from a corrupted "
                          "handle, so rt_ipc_open fails (open-fails): every rank must take the torch.distributed "
-                         "gather")
+                         "gather; or it finishes its set-up --slow-setup-s seconds late (slow-setup: past the "
+                         "exchange bound; the ranks start the warm-up together, so the run must complete on the "
+                         "IPC exchange)")
+    ap.add_argument("--slow-setup-s", type=float, default=3.0, help="the slow-setup fault's delay")
+    ap.add_argument("--no-setup-barrier", action="store_true",
+                    help="test only: leave out the barrier before the warm-up (the round-4 flow), so a late rank's "
+                         "set-up eats into rank 0's bounded wait for the first frame")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="raise GPU_MAX_HW_QUEUES to at least this before HIP starts (frames in flight need a "
                          "hardware queue each, beside torch's and RCCL's streams); 0 = keep the inherited value")
@@ -643,8 +650,17 @@ def run(args, world, result_out=None):
     # first frame waits (bounded by --sync-timeout-ms) for every rank's first put, so a rank still
     # finishing its set-up must not eat into that bound.
     torch.cuda.synchronize(dev)
+    if args.inject_fault == "slow-setup" and rank == world - 1 and world > 1:
+        time.sleep(args.slow_setup_s)   # a late rank (set-up slower than the exchange bound)
+    setup_skew = None
     if use_dist:
-        dist.barrier()
+        # when this rank finished its set-up (wall clock of the one host), through the store so that
+        # publishing it synchronises nothing; rank 0 reads every rank's at the end: how far apart
+        # the ranks were, i.e. what the barrier below absorbs and what the first frame's bounded
+        # wait would otherwise see
+        dist.distributed_c10d._get_default_store().set(f"rtamd_ready_{rank}", repr(time.time()))
+        if not args.no_setup_barrier:
+            dist.barrier()
     for _ in range(args.warmup):
         step()
     drain()
@@ -674,7 +690,7 @@ def run(args, world, result_out=None):
     # tests cannot exercise), every rank moves to the torch.distributed gather and warms up
     # again, and the JSON names why (`band_exchange_fallback`).  Not under the timed-region
     # faults of --inject-fault, which must surface.
-    if ipc and not args.shard and args.inject_fault in ("none", "drop-put-warmup"):
+    if ipc and not args.shard and args.inject_fault in ("none", "drop-put-warmup", "slow-setup"):
         ok, why = 1.0, "a rank could not take part"
         if rank == 0:
             st, presented = fsync.status()
@@ -736,6 +752,11 @@ def run(args, world, result_out=None):
     else:
         rays_local, prim_local = rays_f0 * args.steps, prim_f0 * args.steps
     del hits, tt, rgb
+
+    if use_dist and rank == 0:
+        st_ = dist.distributed_c10d._get_default_store()
+        ready = [float(bytes(st_.get(f"rtamd_ready_{q}")).decode()) for q in range(world)]
+        setup_skew = round(max(ready) - min(ready), 3)
 
     # Frame delivery (ipc): rank 0 observed every frame complete (rt_frame_present), or the run
     # failed.  `value` counts only presented frames.
@@ -1039,6 +1060,7 @@ def run(args, world, result_out=None):
                                      else "torch.distributed gather (RCCL), B frames per gather, + rt_assemble_bands on rank 0's "
                                      "assembly stream"),
                    "band_exchange_fallback": exchange_fallback,
+                   "setup_skew_s": setup_skew,
                    "scene_distribution": (f"rank 0 builds; {scene_bytes} B scene image broadcast over RCCL "
                                           "(rt_scene_image_pack / _load)" if world > 1 else "single rank"),
                    "scene_setup_s": round(scene_s, 3),

@@ -163,6 +163,24 @@ int rt_set_params(rt_ctx* ctx, const rt_params* params);
 int rt_render(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr,
               const rt_aux* aux);
 
+/* raytrace_gpgpu (RayTracer.cpp:330-344) on n GPUs from ONE process (SURVEY.md 7.5, 8b:
+ * the reference has one device and one queue, RayTracer.cpp:2097-2131).  ctxs[0..n-1] are
+ * distinct contexts (one per GPU; the same device may repeat), each holding the scene
+ * (rt_upload_scene, or rt_scene_copy from one that does).  The camera is ctxs[0]'s
+ * (rt_set_params; copied to the others).  The frame is cut into 8-row bands dealt round-robin
+ * (band b -> ctxs[b % n]); every context renders its bands on its own stream and
+ * writes each pixel straight into its row of the host frame: the caller's out_bgr when it is
+ * pinned memory the devices can write (hipHostMalloc, or registered mapped), else a pinned
+ * staging frame of ctxs[0] copied to out_bgr after the join.  Synchronous: returns when every
+ * context is done and out_bgr holds the w*h packed pixels -- the same pixels as rt_render with
+ * the same flags.  n == 1 is rt_render.  Errors are reported on ctxs[0] (rt_last_error). */
+int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,
+                    uint32_t* out_bgr);
+/* Copies src's uploaded scene (its device layouts) into dst: device to device on one GPU,
+ * peer to peer over xGMI between two (hipMemcpyPeer), with no host round trip and no second
+ * BVH build (initRayTrace's upload, RayTracer.cpp:942-984, done once per node).  Synchronous. */
+int rt_scene_copy(rt_ctx* dst, rt_ctx* src);
+
 /* Device-resident variant for benchmarks and multi-GPU: renders this rank's
  * bands (tiling may be NULL = whole frame) into device buffers d_out (and the
  * optional device aux planes), enqueued on `stream` (a hipStream_t, NULL =
@@ -312,6 +330,22 @@ int rt_gather_peak(rt_ctx* ctx, uint32_t table_records, uint32_t iters, float* m
  * following one chain: ms per launch and the number of waves (ms / iters = one dependent
  * iteration of a wave with the chip full). */
 int rt_chase_peak(rt_ctx* ctx, uint32_t table_records, uint32_t iters, uint32_t group, float* ms, uint64_t* waves);
+/* The same chain on `blocks` blocks of 4 waves instead of 8 per CU: blocks = the CU count
+ * gives one wave per SIMD (a lone chain's iteration time on an otherwise idle chip). */
+int rt_chase_latency(rt_ctx* ctx, uint32_t table_records, uint32_t iters, uint32_t group, uint32_t blocks, float* ms,
+                     uint64_t* waves);
+/* Where one frame's time goes (diagnostics): renders a frame (flags as rt_render, default
+ * arithmetic; depth 1, or the wavefront path) on the ctx stream, after the frames already
+ * rendered there (so with the adaptive block order the product uses), with a stamping
+ * instantiation of the same kernels.  words[0] = launches L, words[1..L] = waves per launch,
+ * words[9] / [10] = the frame's kernels / its first launch (HIP events, ns), then from word 16
+ * 8 words per wave, launch after launch, waves in blockIdx * 4 + wave order: s_memrealtime
+ * (100 MHz, low 32 bits) at the wave's start, at the end of its rays and at its end (after the
+ * block epilogue: the longest-first order build in the frame's last block); its main-loop and
+ * wave-uniform-prologue traversal trips; HW_REG_XCC_ID; HW_REG_HW_ID; the tile it rendered (first
+ * launch) or the 64-ray groups it took (bounce launches).  *used_words = words written. */
+int rt_wave_timeline(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* words,
+                     uint64_t cap_words, uint64_t* used_words);
 
 /* Traversals of the last frame that outgrew the fast kernel's LDS stack and
  * restarted in-kernel with the general traversal (same result, slower ray);

@@ -181,6 +181,12 @@ struct Outputs {
     uint64_t local_pixels;
     // measurement instantiation only (rt_fetch_counts): the frame's 8 record-fetch counters
     unsigned long long* fcount;
+    // depth-1 kernel only: out is the whole w x h frame (rt_render_tiled: every context writes
+    // its bands' pixels straight into their rows of one frame); 0: out holds this rank's bands
+    // (rt_tiling order), as for every other kernel
+    uint32_t frame_rows;
+    // diagnostic instantiation only (rt_wave_timeline): per wave {start, end, iterations, hw id}
+    uint32_t* wtime;
 };
 
 __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
@@ -265,6 +271,29 @@ __device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
     if (F.nranks <= 1) return lr;
     const uint32_t band = lr / (uint32_t)F.band_rows, rib = lr % (uint32_t)F.band_rows;
     return (band * (uint32_t)F.nranks + (uint32_t)F.rank) * (uint32_t)F.band_rows + rib;
+}
+
+// Diagnostic instantiation only (rt_wave_timeline, TR = 2): a wave's traversal loop trips,
+// counted by its first active lane in the wave's LDS words c[0] (main loop) and c[1]
+// (wave-uniform prologue).
+__device__ __forceinline__ void timeline_step(uint32_t* c, int which) {
+    if ((uint32_t)(threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) c[which] += 1u;
+}
+// ... and its record (8 words, wave w of the launch): s_memrealtime (100 MHz, low 32 bits) at
+// its start, at the end of its rays and now; the two trip counts; HW_REG_XCC_ID; HW_REG_HW_ID
+// (CU, SIMD, wave slot); a tag (the tile, or the bounce kernel's groups taken).  Stamps go to
+// their own buffer only; nothing the frame computes reads them.
+__device__ __forceinline__ void timeline_store(const Outputs& O, uint32_t w, uint32_t t0, uint32_t t1,
+                                               const uint32_t* c, uint32_t tag) {
+    const uint32_t t2 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63u) == 0) {
+        uint32_t* r = O.wtime + (size_t)w * 8;
+        const uint4 a = make_uint4(t0, t1, t2, c[0]);
+        const uint4 b = make_uint4(c[1], (uint32_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)),
+                                   (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)), tag);
+        reinterpret_cast<uint4*>(r)[0] = a;
+        reinterpret_cast<uint4*>(r)[1] = b;
+    }
 }
 
 __device__ __forceinline__ uint32_t block_tile(const Frame& F) { return F.tile_order[blockIdx.x]; }
@@ -788,11 +817,23 @@ struct rt_ctx {
     std::vector<FrameSlot> slots;
     FrameSlot* last_slot = nullptr;
     uint64_t slot_clock = 0;
-    uint32_t* d_order = nullptr; size_t order_cap = 0;        // static block order (column strips)
-    uint32_t order_tx = 0, order_ty = 0;
+    // static block orders (column strips), one per block grid: the row groups of rt_render and
+    // the contexts of rt_render_tiled may differ in grid, and a grid's table is never rewritten
+    // while a frame may read it (no stream sync to switch grids)
+    struct OrderTab { uint32_t tx, ty; uint32_t* d; };
+    static constexpr size_t kMaxOrders = 16;
+    std::vector<OrderTab> orders;
     uint32_t scene_gen = 0;                                   // bumped by every upload
     int wf_grid[3] = {0, 0, 0};   // persistent wavefront grid per math mode
     struct { bool on = false; unsigned long long* d_counts = nullptr; } trace;   // rt_fetch_counts
+    struct {                                                                    // rt_wave_timeline
+        bool on = false;
+        uint32_t* d_words = nullptr; size_t cap = 0;   // device buffer, words
+        size_t limit = 0, used = 0;                    // words the caller takes, words written
+        std::vector<uint32_t> waves;                   // waves per launch of the frame
+    } tline;
+    bool frame_rows = false;   // rt_render_tiled: d_out is the whole frame (rtk::Outputs::frame_rows)
+    uint32_t* h_stage = nullptr; size_t stage_cap = 0;   // rt_render_tiled: pinned frame for pageable callers
     // rt_render's row groups: one stream (so one frame slot) per group, and the event they start after
     hipStream_t gstream[8] = {};
     hipEvent_t gstart = nullptr;
@@ -955,9 +996,9 @@ template <int M> struct Kernels;
             return fast ? (void*)NS::wf_bounce_kernel<true> : (void*)NS::wf_bounce_kernel<false>;          \
         }                                                                                                  \
         static void* traced(bool next) {                                                                   \
-            return next ? (void*)NS::first_bounce_kernel<true, true, true> : (void*)NS::first_bounce_kernel<true, false, true>; \
+            return next ? (void*)NS::first_bounce_kernel<true, true, 1> : (void*)NS::first_bounce_kernel<true, false, 1>; \
         }                                                                                                  \
-        static void* traced_bounce() { return (void*)NS::wf_bounce_kernel<true, true>; }                  \
+        static void* traced_bounce() { return (void*)NS::wf_bounce_kernel<true, 1>; }                     \
     };
 RTK_KERNELS(0, rtk_strict)
 RTK_KERNELS(1, rtk_hw)
@@ -979,6 +1020,11 @@ static void* kernel_traced_bounce(int m) {
 static void* kernel_bounce(int m, bool fast) {
     return m == 0 ? Kernels<0>::bounce(fast) : m == 1 ? Kernels<1>::bounce(fast) : Kernels<2>::bounce(fast);
 }
+// the timeline instantiation (rt_wave_timeline): S_ref, the fast kernels
+static void* kernel_timeline_first(bool next) {
+    return next ? (void*)rtk_ref::first_bounce_kernel<true, true, 2> : (void*)rtk_ref::first_bounce_kernel<true, false, 2>;
+}
+static void* kernel_timeline_bounce() { return (void*)rtk_ref::wf_bounce_kernel<true, 2>; }
 
 extern "C" {
 
@@ -1136,7 +1182,9 @@ int rt_destroy(rt_ctx* c) {
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_overflow) (void)hipFree(c->d_overflow);
     for (auto& f : c->slots) free_slot(f);
-    if (c->d_order) (void)hipFree(c->d_order);
+    for (auto& o : c->orders) (void)hipFree(o.d);
+    if (c->tline.d_words) (void)hipFree(c->tline.d_words);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (auto& f : c->ring)
         for (hipEvent_t& e : f.e)
             if (e) (void)hipEventDestroy(e);
@@ -1491,7 +1539,18 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
     O.fcount = nullptr;
+    O.frame_rows = c->frame_rows ? 1u : 0u;
+    O.wtime = nullptr;
     const bool traced = c->trace.on;
+    const bool tline = c->tline.on;
+    // rt_wave_timeline: launch k's wave records at the next free words of the device buffer
+    auto tline_region = [&](uint32_t waves) -> uint32_t* {
+        if (c->tline.used + (size_t)waves * 8 > c->tline.limit) return nullptr;
+        uint32_t* p = c->tline.d_words + c->tline.used;
+        c->tline.used += (size_t)waves * 8;
+        c->tline.waves.push_back(waves);
+        return p;
+    };
 
     rt_ctx::FrameEv& E = c->ring[c->frames % rt_ctx::kRing];
     for (hipEvent_t& e : E.e)
@@ -1522,18 +1581,31 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     auto sums = [&](int k) { return cnt + kCounters + (size_t)(k - 1) * (nchunk + nsuper); };   // queue k >= 1
     O.restarts = cnt + kRestartSlot;
 
-    // static block order: a host-built table, rebuilt when the block grid changes
-    if (c->order_tx != F.tiles_x || c->order_ty != F.tiles_y || !c->d_order) {
+    // static block order: a host-built table per block grid, made once (a new table goes into
+    // a new allocation, so frames in flight that read another grid's table never wait)
+    F.tile_order = nullptr;
+    for (const auto& o : c->orders)
+        if (o.tx == F.tiles_x && o.ty == F.tiles_y) F.tile_order = o.d;
+    if (!F.tile_order) {
+        if (c->orders.size() >= rt_ctx::kMaxOrders) {   // many grids: drop them all, once every frame is done
+            HIPC(c, hipStreamSynchronize(s));
+            for (auto& f : c->slots)
+                if (f.idle) HIPC(c, hipEventSynchronize(f.idle));
+            for (auto& o : c->orders) (void)hipFree(o.d);
+            c->orders.clear();
+        }
         const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y);
-        HIPC(c, hipStreamSynchronize(s));   // an earlier frame on this stream may still read the table
-        for (auto& f : c->slots)
-            if (f.idle) HIPC(c, hipEventSynchronize(f.idle));
-        if ((rc = ensure(c, c->d_order, c->order_cap, tab.size()))) return rc;
-        HIPC(c, hipMemcpy(c->d_order, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
-        c->order_tx = F.tiles_x;
-        c->order_ty = F.tiles_y;
+        uint32_t* d = nullptr;
+        size_t cap = 0;
+        if ((rc = ensure(c, d, cap, tab.size()))) return rc;
+        const hipError_t e = hipMemcpy(d, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return set_err(c, std::string("rt_render_device: order table: ") + hipGetErrorString(e), RT_ERR_DEVICE);
+        }
+        c->orders.push_back(rt_ctx::OrderTab{F.tiles_x, F.tiles_y, d});
+        F.tile_order = d;
     }
-    F.tile_order = c->d_order;
     // Adaptive longest-first order from the previous frame of the same geometry on this
     // slot, built by that frame's last block; the first frame runs the static order.
     F.tile_cost = nullptr;
@@ -1609,6 +1681,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             if (traced) {   // rt_fetch_counts: the counting instantiation of the same kernel
                 O.fcount = c->trace.d_counts;
                 HIPC(c, hipLaunchKernel(kernel_traced(math, depth > 1), grid, block, args, 0, s));
+            } else if (tline) {   // rt_wave_timeline: the stamping instantiation
+                if (!(O.wtime = tline_region(F.num_blocks * 4u)))
+                    return set_err(c, "rt_wave_timeline: buffer too small", RT_ERR_INVALID_ARG);
+                HIPC(c, hipLaunchKernel(kernel_timeline_first(depth > 1), grid, block, args, 0, s));
             } else {
                 HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
             }
@@ -1640,8 +1716,13 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             W.fetch = bc + 32;
             W.bounce = k;
             void* args[] = {&S, &Fb, &O, &W, &ax};
-            HIPC(c, hipLaunchKernel(traced ? kernel_traced_bounce(math) : kernel_bounce(math, fast), dim3(c->wf_grid[math]),
-                                    dim3(256), args, 0, s));
+            void* kb = traced ? kernel_traced_bounce(math) : kernel_bounce(math, fast);
+            if (tline) {
+                if (!(O.wtime = tline_region((uint32_t)c->wf_grid[math] * 4u)))
+                    return set_err(c, "rt_wave_timeline: buffer too small", RT_ERR_INVALID_ARG);
+                kb = kernel_timeline_bounce();
+            }
+            HIPC(c, hipLaunchKernel(kb, dim3(c->wf_grid[math]), dim3(256), args, 0, s));
         }
     }
     HIPC(c, hipGetLastError());
@@ -1721,7 +1802,18 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         if (!c->gstream[g]) HIPC(c, hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking));
     // after whatever the ctx's own stream still holds (the synchronous entry points leave it idle)
     if (!c->gstart) HIPC(c, hipEventCreateWithFlags(&c->gstart, hipEventDisableTiming));
+    // The frame's timing entry (rt_last_timing / rt_timing_average): the span from here, on the
+    // ctx stream, to the end of the last group's kernels, joined back to the ctx stream.  The
+    // groups' own entries go into the ring after it and are dropped again below, so one
+    // grouped frame is one timing entry, like any other frame.
+    const uint64_t f0 = c->frames;
+    rt_ctx::FrameEv& FE = c->ring[f0 % rt_ctx::kRing];
+    for (hipEvent_t& e : FE.e)
+        if (!e) HIPC(c, hipEventCreate(&e));
+    FE.has_k = false;
+    HIPC(c, hipEventRecord(FE.e[0], c->stream));
     HIPC(c, hipEventRecord(c->gstart, c->stream));
+    c->frames = f0 + 1;
     std::vector<rt_ctx::FrameSlot*> slots;
     // every group's kernels first, then the readbacks in group order: a copy into pageable
     // memory may block the host until it is done, and the later groups must already be queued
@@ -1731,11 +1823,15 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         const rt_tiling t{(int32_t)g, (int32_t)groups, (int32_t)band_rows, 0};
         const size_t p0 = (size_t)g * band_rows * w;
         rt_aux ga{nullptr, nullptr, nullptr};
-        if (want) ga = rt_aux{c->d_hits + p0 * dd * 2, c->d_t + p0 * dd, c->d_rgb + p0 * 3};
+        if (want) ga = rt_aux{c->d_hits + p0 * depth * 2, c->d_t + p0 * depth, c->d_rgb + p0 * 3};
         rc = rt_render_device(c, w, h, depth, flags, &t, c->d_out + p0, want ? &ga : nullptr, s);
         if (rc) return rc;
         slots.push_back(c->last_slot);
     }
+    for (uint32_t g = 0; g < groups; ++g)   // the frame ends with the last group's kernels
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ring[(f0 + 1 + g) % rt_ctx::kRing].e[1], 0));
+    HIPC(c, hipEventRecord(FE.e[1], c->stream));
+    c->frames = f0 + 1;
     for (uint32_t g = 0; g < groups; ++g) {
         hipStream_t s = c->gstream[g];
         const size_t p0 = (size_t)g * band_rows * w, np = (size_t)std::min<uint64_t>(band_rows, h - (uint64_t)g * band_rows) * w;
@@ -1875,12 +1971,19 @@ int rt_gather_peak(rt_ctx* c, uint32_t table_records, uint32_t iters, float* ms,
 }
 
 int rt_chase_peak(rt_ctx* c, uint32_t table_records, uint32_t iters, uint32_t group, float* ms, uint64_t* waves) {
-    if (!c || !ms || !waves || table_records < 2 || iters == 0 || group == 0 || group > 64 || (64 % group))
+    if (!c) return RT_ERR_INVALID_ARG;
+    int cus = 0;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    return rt_chase_latency(c, table_records, iters, group, (uint32_t)cus * 8u, ms, waves);   // 8 waves per SIMD
+}
+
+int rt_chase_latency(rt_ctx* c, uint32_t table_records, uint32_t iters, uint32_t group, uint32_t blocks, float* ms,
+                     uint64_t* waves) {
+    if (!c || !ms || !waves || table_records < 2 || iters == 0 || group == 0 || group > 64 || (64 % group) ||
+        blocks == 0 || blocks > (1u << 20))
         return set_err(c, "rt_chase_peak: invalid argument", RT_ERR_INVALID_ARG);
     HIPC(c, hipSetDevice(c->device));
-    int cus = 0;
-    HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    const uint32_t blocks = (uint32_t)cus * 8u;   // 8 blocks of 4 waves per CU: 8 waves per SIMD
     // the table: random child references (two per record, both valid), boxes from a fixed pattern
     std::vector<float4> tab((size_t)table_records * 4);
     uint32_t x = 0x9E3779B9u;
@@ -1928,6 +2031,164 @@ int rt_chase_peak(rt_ctx* c, uint32_t table_records, uint32_t iters, uint32_t gr
     if (e != hipSuccess) return set_err(c, std::string("rt_chase_peak: ") + hipGetErrorString(e), RT_ERR_DEVICE);
     *ms = t / 4.0f;
     *waves = (uint64_t)blocks * 4u;
+    return RT_OK;
+}
+
+// ---- one frame on several GPUs, one process (rt_render_tiled) ----
+
+int rt_scene_copy(rt_ctx* dst, rt_ctx* src) {
+    if (!dst || !src) return set_err(dst, "rt_scene_copy: invalid argument", RT_ERR_INVALID_ARG);
+    if (dst == src) return RT_OK;
+    if (!src->have_scene) return set_err(dst, "rt_scene_copy: the source context has no scene", RT_ERR_NO_SCENE);
+    HIPC(dst, hipSetDevice(dst->device));
+    for (auto& f : dst->slots)
+        if (f.idle) HIPC(dst, hipEventSynchronize(f.idle));   // frames in flight still read the old scene
+    free_scene(dst);
+    HIPC(dst, alloc_records(dst, src->n_wnodes4, src->n_tris4));
+    HIPC(dst, hipMalloc((void**)&dst->d_shade, std::max<size_t>(src->n_shade4, 1) * 16));
+    HIPC(dst, hipMalloc((void**)&dst->d_leaf, src->n_leaf * 8));
+    // device to device on one GPU, else peer to peer (xGMI), both on dst's stream
+    const std::pair<std::pair<void*, const void*>, size_t> parts[] = {
+        {{dst->d_wnodes, src->d_wnodes}, src->n_wnodes4 * 16}, {{dst->d_tris, src->d_tris}, src->n_tris4 * 16},
+        {{dst->d_shade, src->d_shade}, src->n_shade4 * 16}, {{dst->d_leaf, src->d_leaf}, src->n_leaf * 8}};
+    for (const auto& q : parts) {
+        if (!q.second) continue;
+        if (dst->device == src->device)
+            HIPC(dst, hipMemcpyAsync(q.first.first, q.first.second, q.second, hipMemcpyDeviceToDevice, dst->stream));
+        else
+            HIPC(dst, hipMemcpyPeerAsync(q.first.first, dst->device, q.first.second, src->device, q.second, dst->stream));
+    }
+    HIPC(dst, hipStreamSynchronize(dst->stream));
+    dst->n_wnodes4 = src->n_wnodes4; dst->n_tris4 = src->n_tris4; dst->n_shade4 = src->n_shade4; dst->n_leaf = src->n_leaf;
+    dst->root = src->root;
+    dst->n_inner = src->n_inner;
+    dst->fast_div = src->fast_div;
+    dst->clean = src->clean;
+    dst->have_scene = true;
+    ++dst->scene_gen;
+    return RT_OK;
+}
+
+// rt_render_tiled: the frame is cut into 8-row bands dealt round-robin over the contexts
+// (rt_tiling).  Every context renders its bands on its own stream with the
+// frame-row output of the kernels (rtk::Outputs::frame_rows): each pixel store goes straight to
+// its place in ONE host frame, so every GPU sends its own rows over its own host link while it
+// renders, and there is no gather, copy or re-interleave step.  That frame is the caller's
+// buffer when it is pinned memory the devices can write, else ctx 0's pinned staging frame,
+// copied to the caller's memory after the join.  Then every stream is synchronised: returns
+// with the frame complete in out_bgr, like raytrace_gpgpu (RayTracer.cpp:330-344).
+constexpr int32_t kTiledBandRows = 8;
+constexpr int32_t kMaxTiled = 64;
+
+int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr) {
+    if (!ctxs || n < 1 || n > kMaxTiled || !out_bgr || w == 0 || h == 0 || depth < 0 || depth > RT_MAX_DEPTH)
+        return set_err(nullptr, "rt_render_tiled: invalid argument", RT_ERR_INVALID_ARG);
+    for (int32_t k = 0; k < n; ++k) {
+        if (!ctxs[k]) return set_err(nullptr, "rt_render_tiled: ctxs[k] is NULL", RT_ERR_INVALID_ARG);
+        for (int32_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return set_err(nullptr, "rt_render_tiled: a context appears twice", RT_ERR_INVALID_ARG);
+    }
+    rt_ctx* c0 = ctxs[0];
+    if ((flags & RT_FLAG_STRICT_MATH) && (flags & RT_FLAG_HW_MATH))
+        return set_err(c0, "rt_render_tiled: RT_FLAG_STRICT_MATH and RT_FLAG_HW_MATH exclude each other", RT_ERR_INVALID_ARG);
+    if (!c0->have_params) return set_err(c0, "rt_render_tiled: no params set on ctxs[0]", RT_ERR_NO_SCENE);
+    for (int32_t k = 0; k < n; ++k)
+        if (!ctxs[k]->have_scene)
+            return set_err(c0, "rt_render_tiled: ctxs[" + std::to_string(k) + "] has no scene (rt_scene_copy)", RT_ERR_NO_SCENE);
+    if (n == 1) return rt_render(c0, w, h, depth, flags, out_bgr, nullptr);
+    const size_t npix = (size_t)w * h;
+    HIPC(c0, hipSetDevice(c0->device));
+    uint32_t* frame = nullptr;
+    bool staged = false;
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, out_bgr) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer &&
+        !((uintptr_t)pa.devicePointer & 15u)) {   // (16-B aligned: the row-copy kernel's stores)
+        frame = (uint32_t*)pa.devicePointer;
+    } else {
+        staged = true;
+        (void)hipGetLastError();   // pageable memory: not an error
+        if (c0->stage_cap < npix) {
+            if (c0->h_stage) (void)hipHostFree(c0->h_stage);
+            c0->h_stage = nullptr;
+            c0->stage_cap = 0;
+            HIPC(c0, hipHostMalloc((void**)&c0->h_stage, npix * 4, hipHostMallocPortable | hipHostMallocMapped));
+            c0->stage_cap = npix;
+        }
+        void* dp = nullptr;
+        HIPC(c0, hipHostGetDevicePointer(&dp, c0->h_stage, 0));
+        frame = (uint32_t*)dp;
+    }
+    int rc = RT_OK;
+    int32_t queued = 0;
+    for (; queued < n; ++queued) {
+        rt_ctx* c = ctxs[queued];
+        if (queued) {
+            c->params = c0->params;   // ctxs[0]'s camera drives the frame (updateCamera, RayTracer.cpp:671)
+            c->have_params = true;
+        }
+        const rt_tiling t{queued, n, kTiledBandRows, 0};
+        if (depth == 1) {   // the depth-1 kernel writes its pixels into the frame's rows itself
+            c->frame_rows = true;
+            rc = rt_render_device(c, w, h, depth, flags, &t, frame, nullptr, c->stream);
+            c->frame_rows = false;
+        } else {            // other kernels: the context's bands, then one row-copy kernel into the frame
+            const int64_t lp = rt_tiling_pixels(w, h, &t);
+            if (lp > 0 && (rc = ensure(c, c->d_out, c->out_cap, (size_t)lp)) == RT_OK &&
+                (rc = rt_render_device(c, w, h, depth, flags, &t, c->d_out, nullptr, c->stream)) == RT_OK &&
+                rt_bands_put(c->d_out, frame, w, h, &t, c->stream) != RT_OK)
+                rc = set_err(c, g_err, RT_ERR_DEVICE);
+        }
+        if (rc) {
+            if (c != c0) c0->err = "rt_render_tiled: ctxs[" + std::to_string(queued) + "]: " + c->err;
+            break;
+        }
+    }
+    // join: every context that has work queued, also after a failure (nothing may still write
+    // into the frame when this returns)
+    for (int32_t k = 0; k < queued; ++k) {
+        rt_ctx* c = ctxs[k];
+        const hipError_t e = hipSetDevice(c->device) == hipSuccess ? hipStreamSynchronize(c->stream) : hipErrorInvalidDevice;
+        if (e != hipSuccess && rc == RT_OK)
+            rc = set_err(c0, "rt_render_tiled: ctxs[" + std::to_string(k) + "]: " + hipGetErrorString(e), RT_ERR_DEVICE);
+    }
+    (void)hipSetDevice(c0->device);
+    if (rc) return rc;
+    if (staged) std::memcpy(out_bgr, c0->h_stage, npix * 4);
+    return RT_OK;
+}
+
+// ---- diagnostics: where a frame's time goes ----
+
+int rt_wave_timeline(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* words,
+                     uint64_t cap_words, uint64_t* used_words) {
+    if (!c || !words || !used_words || cap_words < 16 || w == 0 || h == 0 || depth < 1 || depth > RT_MAX_DEPTH)
+        return set_err(c, "rt_wave_timeline: invalid argument", RT_ERR_INVALID_ARG);
+    if ((flags & (RT_FLAG_STRICT_MATH | RT_FLAG_HW_MATH | RT_FLAG_EXACT_DIV)) || (depth > 1 && !(flags & RT_FLAG_WAVEFRONT)) ||
+        !c->have_scene || !c->clean || c->split_records)
+        return set_err(c, "rt_wave_timeline: the default arithmetic's fast kernels of a clean scene, depth 1 or the wavefront path",
+                       RT_ERR_INVALID_ARG);
+    HIPC(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->d_out, c->out_cap, (size_t)w * h);
+    if (rc) return rc;
+    if ((rc = ensure(c, c->tline.d_words, c->tline.cap, (size_t)cap_words))) return rc;
+    HIPC(c, hipMemsetAsync(c->tline.d_words, 0, (size_t)cap_words * 4, c->stream));
+    c->tline.on = true;
+    c->tline.limit = (size_t)cap_words - 16;
+    c->tline.used = 0;
+    c->tline.waves.clear();
+    rc = rt_render_device(c, w, h, depth, flags, nullptr, c->d_out, nullptr, c->stream);
+    c->tline.on = false;
+    if (rc) return rc;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    float t = 0.0f, k = 0.0f;
+    if ((rc = frame_times(c, c->frames - 1, t, k))) return rc;
+    std::memset(words, 0, 16 * 4);
+    words[0] = (uint32_t)c->tline.waves.size();
+    for (size_t i = 0; i < c->tline.waves.size() && i < 8; ++i) words[1 + i] = c->tline.waves[i];
+    words[9] = (uint32_t)std::lround((double)t * 1e6);   // the frame's kernels, HIP events, ns
+    words[10] = (uint32_t)std::lround((double)k * 1e6);  // its first launch
+    HIPC(c, hipMemcpy(words + 16, c->tline.d_words, c->tline.used * 4, hipMemcpyDeviceToHost));
+    *used_words = 16 + c->tline.used;
     return RT_OK;
 }
 

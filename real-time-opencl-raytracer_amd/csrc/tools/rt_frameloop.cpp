@@ -5,11 +5,13 @@
 // fixed per-frame drag instead of a mouse.  Frames go through the C ABI exactly
 // as the reference's host path does: rt_set_params (clEnqueueWriteBuffer of
 // Params, :671) then rt_render (launch + finish + blocking read-back, :330-344).
-// Optional PPM dumps replace the window.
+// Optional PPM dumps replace the window.  With --gpus N (devices 0..N-1) or --devices a,b,...
+// (a list; a device may repeat) every frame goes to rt_render_tiled over one context per
+// entry instead: the scene is uploaded once and copied to the others (rt_scene_copy).
 //
 //   rt_frameloop [--dae F | --obj F | --scene cornell|knot|heightfield] [--bvh-cache F]
 //                [--width W] [--height H] [--depth D] [--frames N] [--drag DX DY]
-//                [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F]
+//                [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F] [--gpus N | --devices a,b,...]
 //
 // Prints "N.N fps" lines and a final JSON summary.
 #include <chrono>
@@ -30,13 +32,15 @@ struct Args {
     int depth = 3, frames = 120, ppm_every = 0, device = 0;
     uint32_t flags = 0;
     float dx = 4.0f, dy = 0.0f;
+    std::vector<int> devices;   // rt_render_tiled over these (empty: rt_render on --device)
 };
 
 int usage() {
     std::fprintf(stderr,
                  "usage: rt_frameloop [--dae F | --obj F | --scene cornell|knot|heightfield] [--bvh-cache F]\n"
                  "                    [--width W] [--height H] [--depth D] [--frames N] [--drag DX DY]\n"
-                 "                    [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F]\n");
+                 "                    [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F]\n"
+                 "                    [--gpus N | --devices a,b,...]\n");
     return 2;
 }
 
@@ -57,7 +61,23 @@ bool parse(int argc, char** argv, Args& a) {
         else if (k == "--ppm-every" && need(1)) a.ppm_every = std::atoi(argv[++i]);
         else if (k == "--device" && need(1)) a.device = std::atoi(argv[++i]);
         else if (k == "--flags" && need(1)) a.flags = (uint32_t)std::strtoul(argv[++i], nullptr, 0);
-        else return false;
+        else if (k == "--gpus" && need(1)) {
+            const int n = std::atoi(argv[++i]);
+            if (n < 1 || n > 64) return false;
+            a.devices.clear();
+            for (int d = 0; d < n; ++d) a.devices.push_back(d);
+        } else if (k == "--devices" && need(1)) {
+            a.devices.clear();
+            for (const char* p = argv[++i]; *p;) {
+                char* end = nullptr;
+                const long d = std::strtol(p, &end, 10);
+                if (end == p || d < 0) return false;
+                a.devices.push_back((int)d);
+                p = *end == ',' ? end + 1 : end;
+                if (*end && *end != ',') return false;
+            }
+            if (a.devices.empty() || a.devices.size() > 64) return false;
+        } else return false;
     }
     return a.w > 0 && a.h > 0 && a.frames > 0 && a.depth >= 0 && a.depth <= RT_MAX_DEPTH;
 }
@@ -112,12 +132,25 @@ int main(int argc, char** argv) {
     rt_bvh_view bv;
     rt_mesh_view_get(mesh, &mv);
     rt_bvh_view_get(bvh, &bv);
-    rt_ctx* ctx = nullptr;
-    if ((rc = rt_create(a.device, &ctx)) != RT_OK) { std::fprintf(stderr, "rt_create: %s\n", rt_last_error(nullptr)); return 1; }
+    // one context per GPU entry (a single one on --device without --gpus / --devices)
+    if (a.devices.empty()) a.devices.push_back(a.device);
+    std::vector<rt_ctx*> ctxs(a.devices.size(), nullptr);
+    for (size_t k = 0; k < ctxs.size(); ++k)
+        if ((rc = rt_create(a.devices[k], &ctxs[k])) != RT_OK) {
+            std::fprintf(stderr, "rt_create(%d): %s\n", a.devices[k], rt_last_error(nullptr));
+            return 1;
+        }
+    rt_ctx* ctx = ctxs[0];
     rc = rt_upload_scene(ctx, mv.vertices, mv.num_vertices, mv.indices, mv.num_indices, bv.nodes, bv.num_nodes,
                          bv.tri_indices, bv.num_tri_indices, mv.normals, mv.num_normals, mv.normals_indices,
                          mv.materials, mv.num_materials, mv.tri_to_material);
     if (rc != RT_OK) { std::fprintf(stderr, "rt_upload_scene: %s\n", rt_last_error(ctx)); return 1; }
+    for (size_t k = 1; k < ctxs.size(); ++k)   // the scene once per node: copied, not re-uploaded
+        if ((rc = rt_scene_copy(ctxs[k], ctx)) != RT_OK) {
+            std::fprintf(stderr, "rt_scene_copy: %s\n", rt_last_error(ctxs[k]));
+            return 1;
+        }
+    const int32_t nctx = (int32_t)ctxs.size();
 
     rt_camera* cam = rt_camera_create(200.0f);
     std::vector<uint32_t> px((size_t)a.w * a.h);
@@ -129,7 +162,8 @@ int main(int argc, char** argv) {
         rt_params p;
         rt_camera_frame_params(cam, mesh, a.w, a.h, nullptr, nullptr, &p);   // updateCamera()
         if ((rc = rt_set_params(ctx, &p)) != RT_OK ||
-            (rc = rt_render(ctx, a.w, a.h, a.depth, a.flags, px.data(), nullptr)) != RT_OK) {
+            (rc = nctx > 1 ? rt_render_tiled(ctxs.data(), nctx, a.w, a.h, a.depth, a.flags, px.data())
+                           : rt_render(ctx, a.w, a.h, a.depth, a.flags, px.data(), nullptr)) != RT_OK) {
             std::fprintf(stderr, "frame %d: %s\n", f, rt_last_error(ctx));
             return 1;
         }
@@ -154,11 +188,11 @@ int main(int argc, char** argv) {
     const double wall = std::chrono::duration<double>(clk::now() - t0).count();
     std::printf("{\"frames\": %d, \"width\": %u, \"height\": %u, \"depth\": %d, \"fps\": %.2f, \"ms_per_frame\": %.4f, "
                 "\"kernel_ms_per_frame\": %.4f, \"triangles\": %d, \"bvh_nodes\": %d, \"bvh_cached\": %s, "
-                "\"bvh_seconds\": %.3f}\n",
+                "\"bvh_seconds\": %.3f, \"contexts\": %d}\n",
                 total, a.w, a.h, a.depth, total / wall, 1e3 * wall / total, kernel_ms_sum / total,
-                mv.num_indices / 3, bv.num_nodes, cached ? "true" : "false", bvh_s);
+                mv.num_indices / 3, bv.num_nodes, cached ? "true" : "false", bvh_s, nctx);
     rt_camera_destroy(cam);
-    rt_destroy(ctx);
+    for (rt_ctx* c : ctxs) rt_destroy(c);
     rt_bvh_destroy(bvh);
     rt_mesh_destroy(mesh);
     return 0;

@@ -80,14 +80,15 @@ class rt_bvh_view(C.Structure):
 
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
-ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_device",
+ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_tiled", "rt_scene_copy",
+               "rt_render_device",
                "rt_tiling_pixels", "rt_assemble_bands", "rt_assemble_bands_batch", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
                "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
                "rt_frame_ready_wait", "rt_ipc_export", "rt_ipc_open", "rt_ipc_close", "rt_bands_put",
                "rt_peer_access", "rt_frame_sync_words", "rt_bands_put_sync", "rt_frame_present", "rt_frame_release",
                "rt_frame_sync_status", "rt_frame_checksum", "rt_shared_alloc", "rt_shared_free", "rt_copy_device",
                "rt_scene_image_size", "rt_scene_image_pack",
-               "rt_scene_image_load", "rt_fetch_counts", "rt_gather_peak", "rt_chase_peak", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
+               "rt_scene_image_load", "rt_fetch_counts", "rt_gather_peak", "rt_chase_peak", "rt_chase_latency", "rt_wave_timeline", "rt_last_timing", "rt_timing_average", "rt_last_deferred", "rt_overflow_count", "rt_destroy", "rt_last_error",
                "rt_abi_version"]
 HOST_SYMBOLS = ["rt_mesh_create", "rt_mesh_destroy", "rt_mesh_view_get", "rt_mesh_set", "rt_mesh_load_obj",
                 "rt_mesh_load_dae", "rt_mesh_save_dae",
@@ -119,6 +120,8 @@ def lib() -> C.CDLL:
             "rt_upload_scene": (C.c_int, [vp, vp, i32, vp, i32, vp, i32, vp, i32, vp, i32, vp, vp, i32, vp]),
             "rt_set_params": (C.c_int, [vp, C.POINTER(rt_params)]),
             "rt_render": (C.c_int, [vp, u32, u32, i32, u32, vp, C.POINTER(rt_aux)]),
+            "rt_render_tiled": (C.c_int, [C.POINTER(vp), i32, u32, u32, i32, u32, vp]),
+            "rt_scene_copy": (C.c_int, [vp, vp]),
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
             "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
             "rt_assemble_bands": (C.c_int, [vp, vp, C.c_uint64, u32, u32, i32, i32, vp]),
@@ -151,6 +154,8 @@ def lib() -> C.CDLL:
             "rt_fetch_counts": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(C.c_uint64)]),
             "rt_gather_peak": (C.c_int, [vp, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
             "rt_chase_peak": (C.c_int, [vp, u32, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
+            "rt_chase_latency": (C.c_int, [vp, u32, u32, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
+            "rt_wave_timeline": (C.c_int, [vp, u32, u32, i32, u32, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
             "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
             "rt_last_deferred": (C.c_int, [vp, C.POINTER(u32)]),
@@ -481,6 +486,42 @@ class Renderer:
         _check(lib().rt_chase_peak(self._h, table_records, iters, group, C.byref(ms), C.byref(waves)), self._h)
         return ms.value, waves.value
 
+    def chase_latency(self, blocks: int, table_records: int = 16384, iters: int = 512, group: int = 4):
+        """rt_chase_latency: the chase chain on `blocks` blocks of 4 waves (blocks = CUs: one wave
+        per SIMD) -> (ms per launch, waves)."""
+        ms, waves = C.c_float(), C.c_uint64()
+        _check(lib().rt_chase_latency(self._h, table_records, iters, group, blocks, C.byref(ms), C.byref(waves)),
+               self._h)
+        return ms.value, waves.value
+
+    def wave_timeline(self, w: int, h: int, depth: int = 1, flags: int = 0, cap_words: int = 1 << 24):
+        """rt_wave_timeline: one frame with per-wave stamps.  Returns {"frame_ns", "first_ns", "launches":
+        [structured array per launch: t0, t1, t2 (10 ns ticks, relative to the frame's first wave
+        start), main, prologue (loop trips), xcc, hwid, tag]}."""
+        buf = np.zeros(cap_words, np.uint32)
+        used = C.c_uint64()
+        _check(lib().rt_wave_timeline(self._h, w, h, depth, flags, _ptr(buf), cap_words, C.byref(used)), self._h)
+        nl = int(buf[0])
+        recs, off = [], 16
+        for k in range(nl):
+            nw = int(buf[1 + k])
+            recs.append(buf[off:off + nw * 8].reshape(nw, 8).copy())
+            off += nw * 8
+        base = min(int(r[:, 0].min()) for r in recs) if recs else 0
+        out = []
+        for r in recs:
+            a = r.astype(np.int64)
+            for j in range(3):   # 32-bit tick wrap: relative to the first start
+                a[:, j] = (r[:, j].astype(np.int64) - base) & 0xFFFFFFFF
+            out.append({"t0": a[:, 0], "t1": a[:, 1], "t2": a[:, 2], "main": a[:, 3], "prologue": a[:, 4],
+                        "xcc": a[:, 5] & 0xF, "hwid": a[:, 6], "tag": a[:, 7]})
+        return {"frame_ns": int(buf[9]), "first_ns": int(buf[10]), "launches": out}
+
+    def copy_scene_from(self, src: "Renderer") -> None:
+        """rt_scene_copy: this ctx gets src's uploaded scene (device to device / peer to peer)."""
+        self._scene_keepalive = None
+        _check(lib().rt_scene_copy(self._h, src._h), self._h)
+
     def gather_peak(self, table_records: int = 16384, iters: int = 256):
         """rt_gather_peak: (ms per launch, records read) of the random-record gather ceiling."""
         ms, n = C.c_float(), C.c_uint64()
@@ -563,6 +604,23 @@ class Renderer:
         v = C.c_uint64()
         _check(lib().rt_overflow_count(self._h, C.byref(v)), self._h)
         return v.value
+
+
+def render_tiled(renderers, w: int, h: int, depth: int = 3, flags: int = 0, out=None):
+    """rt_render_tiled: one frame over the renderers' GPUs (8-row bands dealt round-robin, every
+    context writing its rows straight into one host frame), synchronous.  `out`: None (a new
+    pageable array), a numpy uint32 array, or an int address of w*h uint32 of host memory
+    (pinned memory is written by the devices directly).  Returns the frame (numpy) or None for
+    an address."""
+    n = len(renderers)
+    arr = (C.c_void_p * max(n, 1))(*[r._h.value if isinstance(r._h, C.c_void_p) else r._h for r in renderers])
+    if out is None:
+        out = np.zeros(w * h, np.uint32)
+    ptr = out if isinstance(out, int) else _ptr(out)
+    rc = lib().rt_render_tiled(arr, n, w, h, depth, flags, ptr)
+    if rc:
+        _check(rc, renderers[0]._h if n else None)
+    return None if isinstance(out, int) else out
 
 
 def tiling_pixels(w: int, h: int, rank: int, nranks: int, band_rows: int) -> int:

@@ -66,3 +66,29 @@ def test_product_has_no_oracle_dependency():
         for f in files:
             if f.endswith((".py", ".cpp", ".hip", ".h", ".inc", "Makefile")):
                 assert not uses.search(open(os.path.join(root, f)).read()), f
+
+
+def test_multi_gpu_and_diagnostic_entry_points_reject_bad_arguments_without_gpu():
+    """rt_render_tiled / rt_scene_copy / rt_wave_timeline / rt_chase_latency validate their
+    arguments before any device call (RT_ERR_INVALID_ARG = -1, message in rt_last_error)."""
+    import numpy as np
+    lib = rtamd.lib()
+    out = np.zeros(64, np.uint32)
+    po = out.ctypes.data_as(C.c_void_p)
+    two = (C.c_void_p * 2)()                       # two NULL contexts
+    assert lib.rt_render_tiled(None, 1, 8, 8, 1, 0, po) == -1
+    assert lib.rt_render_tiled(two, 0, 8, 8, 1, 0, po) == -1     # n = 0
+    assert lib.rt_render_tiled(two, 65, 8, 8, 1, 0, po) == -1    # n > 64
+    assert lib.rt_render_tiled(two, 2, 8, 8, 1, 0, po) == -1     # NULL entries
+    assert b"NULL" in lib.rt_last_error(None)
+    fake = (C.c_void_p * 2)(0x1000, 0x1000)        # never dereferenced: refused as a duplicate first
+    assert lib.rt_render_tiled(fake, 2, 8, 8, 1, 0, po) == -1
+    assert b"twice" in lib.rt_last_error(None)
+    assert lib.rt_render_tiled(two, 2, 8, 8, 1, 0, None) == -1   # no output
+    assert lib.rt_render_tiled(two, 2, 0, 8, 1, 0, po) == -1     # zero width
+    assert lib.rt_render_tiled(two, 2, 8, 8, 9, 0, po) == -1     # depth > RT_MAX_DEPTH
+    assert lib.rt_scene_copy(None, None) == -1
+    used = C.c_uint64()
+    assert lib.rt_wave_timeline(None, 8, 8, 1, 0, po, 64, C.byref(used)) == -1
+    ms, waves = C.c_float(), C.c_uint64()
+    assert lib.rt_chase_latency(None, 16, 4, 4, 1, C.byref(ms), C.byref(waves)) == -1

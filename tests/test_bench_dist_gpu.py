@@ -67,7 +67,7 @@ def _ranks_on_one_gpu(n, extra, timeout=115):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--gather", "ipc", "--pg", "gloo",
            "--config", "c2", "--direct", "--warmup", "2", "--warmup-seconds", "0", "--no-cpu-baseline",
-           "--cpu-seconds", "0.5", "--hang-timeout", "100", "--sync-timeout-ms", "30000"] + extra
+           "--cpu-seconds", "0.5", "--hang-timeout", "100"] + extra   # the production exchange bound (10 s)
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
 
@@ -87,6 +87,33 @@ def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
     assert fc["presented_frames_checksummed"] == 26 and fc["checksum_mismatches"] == 0
     assert fc["held_frames_checked"] == 8 and fc["distinct_cameras"] == 26
     assert res["config"]["gathered_frame_equals_single_rank_render"] is True
+    assert res["config"]["setup_skew_s"] is not None and res["config"]["band_exchange_fallback"] is None
+    print(f"{n} ranks: set-up skew {res['config']['setup_skew_s']} s")
+
+
+@pytest.mark.parametrize("barrier", [True, False])
+def test_a_late_rank_at_set_up(barrier):
+    """The round-4 abort's set-up hypothesis, made deterministic: the last of 3 ranks
+    finishes its set-up 3 s late, past a 1.5 s exchange bound.  With the barrier before the warm-up
+    (the fix) the run completes on the IPC exchange, every frame presented; without it (the
+    round-4 flow, --no-setup-barrier) rank 0's bounded wait for the first frame times out, and the
+    warm-up check moves every rank to the RCCL gather -- the run still completes with exit 0, so a
+    late set-up was not what aborted rank 0 with status 1."""
+    extra = ["--steps", "8", "--orbit", "0.01", "--frame-check", "every", "--sync-timeout-ms", "1500",
+             "--inject-fault", "slow-setup", "--slow-setup-s", "3"] + ([] if barrier else ["--no-setup-barrier"])
+    p = _ranks_on_one_gpu(3, extra)
+    assert p.returncode == 0, _why(p)
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = res["config"]
+    assert cfg["setup_skew_s"] >= 2.5, cfg["setup_skew_s"]
+    assert cfg["gathered_frame_equals_single_rank_render"] is True
+    if barrier:
+        assert cfg["band_exchange_fallback"] is None and "rt_bands_put" in cfg["band_exchange"]
+        assert cfg["frame_delivery"]["status"] == 0
+        assert cfg["frame_check"]["checksum_mismatches"] == 0
+    else:
+        assert "warm-up frame delivery: status 2" in cfg["band_exchange_fallback"], cfg["band_exchange_fallback"]
+        assert "torch.distributed gather" in cfg["band_exchange"]
 
 
 def test_frame_check_catches_a_band_from_another_frame():

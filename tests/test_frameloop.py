@@ -22,8 +22,9 @@ def _read_ppm(path):
 
 def test_tool_is_built_and_checks_arguments():
     assert os.access(TOOL, os.X_OK), "build() must produce lib/rt_frameloop"
-    r = subprocess.run([TOOL, "--width", "0"], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 2 and "usage" in r.stderr
+    for bad in (["--width", "0"], ["--gpus", "0"], ["--gpus", "65"], ["--devices", "0,x"], ["--devices", ""]):
+        r = subprocess.run([TOOL, *bad], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 2 and "usage" in r.stderr, bad
 
 
 def test_camera_orbit_matches_repeated_add_rotate():
@@ -40,14 +41,15 @@ def test_camera_orbit_matches_repeated_add_rotate():
     assert np.array_equal(rtamd.params_to_array(c2.params(m, 64, 48)), single)
 
 
-def _run_tool(tmp_path, w, h, depth, frames, dx, dy, flags):
+def _run_tool(tmp_path, w, h, depth, frames, dx, dy, flags, extra=()):
     r = subprocess.run([TOOL, "--scene", "cornell", "--width", str(w), "--height", str(h), "--depth", str(depth),
                         "--frames", str(frames), "--drag", str(dx), str(dy), "--ppm-dir", str(tmp_path),
-                        "--ppm-every", "2", "--bvh-cache", str(tmp_path / "bvh.cache"), "--flags", str(flags)],
-                       capture_output=True, text=True, timeout=300)
+                        "--ppm-every", "2", "--bvh-cache", str(tmp_path / "bvh.cache"), "--flags", str(flags),
+                        *extra], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["frames"] == frames and summary["fps"] > 0
+    return summary
 
 
 def _orbit_params(m, w, h, frames, dx, dy):
@@ -105,3 +107,23 @@ def test_frames_match_the_render_abi(tmp_path):
     r2 = subprocess.run([TOOL, "--scene", "cornell", "--width", str(w), "--height", str(h), "--frames", "2",
                          "--bvh-cache", str(tmp_path / "bvh.cache")], capture_output=True, text=True, timeout=300)
     assert r2.returncode == 0 and json.loads(r2.stdout.strip().splitlines()[-1])["bvh_cached"] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [1, 3])
+def test_multi_context_frames_match_the_render_abi(tmp_path, depth):
+    """--devices 0,0,0: three contexts (device 0 repeated on the one-GPU box) render every frame
+    through rt_render_tiled; the frames equal rt_render's for the same orbiting camera."""
+    import rtamd
+    w, h, frames, dx, dy = 160, 120, 5, 7.0, -3.0
+    summary = _run_tool(tmp_path, w, h, depth, frames, dx, dy, 0, extra=("--devices", "0,0,0"))
+    assert summary["contexts"] == 3
+    m = rtamd.Mesh.cornell()
+    ren = rtamd.Renderer(0)
+    ren.upload(rtamd.Scene.from_mesh(m, m.build_sbvh()))
+    for f, p in enumerate(_orbit_params(m, w, h, frames, dx, dy)):
+        if f % 2:
+            continue
+        ren.set_params(p)
+        assert np.array_equal(_read_ppm(tmp_path / f"frame_{f:05d}.ppm"), _rgb(ren.render(w, h, depth=depth), w, h)), f
+    ren.close()

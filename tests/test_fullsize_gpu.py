@@ -123,25 +123,33 @@ def test_default_math_matches_reference_kernel(renderer, name, tmp_path):
         assert np.array_equal(d1["t"][:, 0].view(np.uint32), d3["t"][:, 0].view(np.uint32))
         if not cfg["flags"] & 1:   # with the shadow ray: the same shadow hits
             assert np.array_equal(d1["hits"][:, 0, 1], d3["hits"][:, 0, 1])
-        if not cfg["flags"] & 1:
-            _pin_depth1_pixels(name, d3, d1["out"], ref)
+        # the benched pixels themselves: with the shadow ray (C3) on every pixel whose depth-3 trace
+        # stopped after one hit; primary-only (C2, RT_FLAG_NO_SHADOW) where, in addition, that hit's
+        # shadow any-hit missed (coefficient 1 in both frames)
+        _pin_depth1_pixels(name, d3, d1["out"], ref, unshadowed=bool(cfg["flags"] & 1))
 
 
-def _pin_depth1_pixels(label, d3, out1, ref):
+def _pin_depth1_pixels(label, d3, out1, ref, unshadowed=False):
     """The benched depth-1 pixels themselves against the reference kernel.  The reference
     always traces RAY_TRACE_DEPTH = 3 bounces (volumeRender.cl:12), but a pixel whose reflected
     ray misses ends with ray_depth = 1, and its packed colour is then color / 1 * shadow / 1
     (volumeRender.cl:1519-1546): exactly the depth-1 frame's.  So on every pixel where the
     pinned depth-3 frame stopped after its first hit (or its primary ray missed: black in
-    both) the depth-1 frame must equal the reference kernel's packed pixel."""
+    both) the depth-1 frame must equal the reference kernel's packed pixel.
+    unshadowed (a primary-only depth-1 frame, RT_FLAG_NO_SHADOW: its shadow coefficient is
+    1): only where the depth-3 frame's bounce-0 shadow any-hit also missed (coefficient 1
+    there too, volumeRender.cl:1437-1460)."""
     h0, h1 = d3["hits"][:, 0, 0], d3["hits"][:, 1, 0]
     one_hit = (h0 >= 0) & (h1 < 0)
+    if unshadowed:
+        one_hit &= d3["hits"][:, 0, 1] < 0
     subset = one_hit | (h0 < 0)
     nd = int(np.sum(out1[subset] != ref[subset]))
-    print(f"{label}: S_ref depth-1 frame vs reference kernel on {int(one_hit.sum())} one-hit pixels "
-          f"(+{int((h0 < 0).sum())} primary misses) of {out1.size}: {nd} differ")
+    print(f"{label}: S_ref depth-1 frame vs reference kernel on {int(one_hit.sum())} one-hit"
+          f"{' unshadowed' if unshadowed else ''} pixels (+{int((h0 < 0).sum())} primary misses) of "
+          f"{out1.size} ({int((h0 >= 0).sum())} scene pixels): {nd} differ")
     assert nd == 0
-    if label.startswith(("c3", "c4")):   # terrain: most reflected rays leave the scene (C1's room keeps them)
+    if label.startswith(("c2", "c3", "c4")):   # most reflected rays leave the scene (C1's room keeps them)
         assert one_hit.sum() > 0.5 * (h0 >= 0).sum(), "the subset covers most of the scene's pixels"
 
 
