@@ -471,7 +471,8 @@ def run(args, world, result_out=None):
     # every, rank 0) each presented frame's checksum, taken on its stream right after the
     # present saw it complete
     frame_of = [[-1] * B for _ in range(NB)]
-    fault = args.inject_fault != "none" and rank == world - 1 and world > 1
+    # the per-frame faults of the last rank (the set-up faults act elsewhere)
+    fault = args.inject_fault in ("wrong-bands", "drop-put", "drop-put-warmup") and rank == world - 1 and world > 1
     fault_frame = 1 if args.inject_fault == "drop-put-warmup" else 4
     check_every = use_dist and rank == 0 and args.frame_check == "every"
     sums = torch.zeros(nframes + args.max_extra_warmup, dtype=torch.int64, device=dev) if check_every else None
@@ -512,11 +513,14 @@ def run(args, world, result_out=None):
         sum_of[cam] = int(ref_sum.item())
         return sum_of[cam]
 
+    held_bad = []   # frame indices of held frames that differ (diagnostics)
+
     def check_held():
         """(frames held, all equal): the frames rank 0's buffer sets hold vs reference()."""
         torch.cuda.synchronize(dev)
         held = [(j, s) for j in range(NB) for s in range(filled[j]) if frame_of[j][s] >= 0]
         ok = bool(held)
+        held_bad.clear()
         for j, s in held:
             reference(frame_of[j][s] % L)
             if ipc:   # the uncached shared frame, copied out
@@ -525,7 +529,11 @@ def run(args, world, result_out=None):
                 got = got_frame
             else:
                 got = frames[j][s]
-            ok = ok and bool(torch.equal(full, got))
+            same = bool(torch.equal(full, got))
+            if not same:
+                held_bad.append({"frame": frame_of[j][s], "set": j, "slot": s,
+                                 "pixels_differ": int((full != got).sum().item())})
+            ok = ok and same
         return len(held), ok
 
     # One step = one frame: render this rank's bands -> (N > 1) RCCL gather of the bands to
@@ -784,7 +792,10 @@ def run(args, world, result_out=None):
             got = sums.cpu().numpy()
             bad = [n for n in checksummed if int(got[n]) != sum_of.get(n % L, None) and
                    int(got[n]) != reference(n % L)]
-            frame_check.update({"presented_frames_checksummed": len(checksummed), "checksum_mismatches": len(bad)})
+            frame_check.update({"presented_frames_checksummed": len(checksummed), "checksum_mismatches": len(bad),
+                                "mismatched_frames": bad[:16]})
+        if held_bad:
+            frame_check["held_frames_differing"] = held_bad[:16]
             frame_ok = frame_ok and not bad
         r.set_params(ptab[0])
 

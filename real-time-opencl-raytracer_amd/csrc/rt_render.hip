@@ -31,8 +31,10 @@
 //  * frame scratch is per stream, so frames enqueued on different streams run
 //    concurrently (frames in flight; multi-GPU band gather overlaps rendering).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -60,6 +62,14 @@
 #endif
 #ifndef RTK_FB_WAVES
 #define RTK_FB_WAVES 8      // waves per SIMD the S_ref depth-1 kernel is bounded to
+#endif
+#ifndef RTK_EXT_EVENTS
+#define RTK_EXT_EVENTS 1    // one-launch frames: timing events from hipExtLaunchKernel, no marker packets
+                            // around the launch (C2 0.0747 vs 0.0764 ms, rt_render into pageable memory 0.527
+                            // vs 0.548 ms; C3, C5 equal: profiles/r05/ab/ext_events_ab.log)
+#endif
+#ifndef RTK_PRIO_BLOCKS
+#define RTK_PRIO_BLOCKS 0   // blocks at the head of the longest-first order that run at wave priority 2
 #endif
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
@@ -107,6 +117,7 @@ struct Frame {
     uint32_t* done;               // blocks finished so far (the last one builds lpt_next)
     uint32_t* zero_next;          // the other parity's frame counters, zeroed by this frame
     uint32_t nzero;
+    uint32_t prio_blocks;         // the first prio_blocks blocks of a longest-first order run at raised wave priority
 };
 
 // A ray in flight between bounces: {pix, o.xyz}, {d.xyz, shadow_sum}, {colour.xyz, 3 * triangle it leaves from}.
@@ -364,9 +375,32 @@ __device__ __forceinline__ uint32_t lpt_key(uint32_t c) {
 // row 1): one lane per block stores its cost write-through (sc1), waits for the store,
 // then adds to one agent-scope counter; the block whose add returns num_blocks - 1 is
 // last, acquires, and reads every cost with sc1 loads.  `scratch` is >= kEpilogueWords
-// words of LDS that no wave uses any more (the traversal stacks).
+// words of LDS that no wave uses any more (the traversal stacks); the rest of it holds the
+// costs' bucket keys, one byte per block, between the two passes (grids of up to kKeyBytes
+// blocks: every BASELINE config at 1080p; larger grids read the costs twice).
+// The last block's sort sits at the very end of the frame, on its critical path: its costs
+// are read 16 per thread per round trip (four 16-B sc1 loads issued together), not one load
+// and one LDS atomic per round trip (RTK_LPT_VEC 0: 2 x 32 dependent L2 round trips for a
+// 1080p frame's 8,160 blocks).
+#ifndef RTK_LPT_VEC
+#define RTK_LPT_VEC 1
+#endif
 constexpr int kEpilogueWords = 8 + 256 + 2 * 256;   // wave times + flag, histogram, two scan rows
 static_assert(4 * kLdsStack * 64 >= kEpilogueWords, "tile_epilogue's scratch must fit the blocks' traversal stacks");
+constexpr uint32_t kKeyBytes = (4u * kLdsStack * 64u - (uint32_t)kEpilogueWords) * 4u;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// costs [4 q, 4 q + 4) .. for q = q0 + u * 256 + tid, u < 4, with four sc1 loads in flight
+// (inline asm: the compiler neither merges nor splits the 16-B agent-scope loads)
+__device__ __forceinline__ void load_costs16(const uint32_t* cost, uint32_t q0, uint32_t nq, u32x4 (&v)[4]) {
+    const u32x4* c4 = reinterpret_cast<const u32x4*>(cost);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const u32x4* p = c4 + min(q0 + (uint32_t)u * 256u + threadIdx.x, nq - 1u);   // in range (a repeat if past)
+        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[u]) : "v"(p) : "memory");
+    }
+    // the wait "writes" the four results, so no use of them is scheduled above it
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : : "memory");
+}
 __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uint32_t* scratch) {
     if (!F.tile_cost) return;   // launch-uniform
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -389,8 +423,35 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
     const uint32_t nb = F.num_blocks;
     hist[tid] = 0;
     __syncthreads();
+#if RTK_LPT_VEC
+    uint8_t* kb = reinterpret_cast<uint8_t*>(scratch + kEpilogueWords);
+    const bool keep = nb <= kKeyBytes;
+    const uint32_t nq = nb >> 2;   // whole 16-B groups of costs
+    for (uint32_t q0 = 0; q0 < nq; q0 += 4u * 256u) {
+        u32x4 v[4];
+        load_costs16(F.tile_cost, q0, nq, v);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t q = q0 + (uint32_t)u * 256u + tid;
+            if (q < nq) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t k = lpt_key(v[u][j]);
+                    atomicAdd(&hist[k], 1u);
+                    if (keep) kb[4u * q + (uint32_t)j] = (uint8_t)k;
+                }
+            }
+        }
+    }
+    for (uint32_t i = 4u * nq + tid; i < nb; i += 256u) {
+        const uint32_t k = lpt_key(__hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        atomicAdd(&hist[k], 1u);
+        if (keep) kb[i] = (uint8_t)k;
+    }
+#else
     for (uint32_t i = tid; i < nb; i += 256)
         atomicAdd(&hist[lpt_key(__hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))], 1u);
+#endif
     __syncthreads();
     // exclusive prefix over the buckets, largest key first (Hillis-Steele on 256 lanes)
     scan[tid] = hist[255 - tid];
@@ -403,10 +464,33 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
     }
     hist[255 - tid] = scan[src * 256 + tid] - hist[255 - tid];   // inclusive -> exclusive
     __syncthreads();
+#if RTK_LPT_VEC
+    if (keep) {
+        for (uint32_t i = tid; i < nb; i += 256u) F.lpt_next[atomicAdd(&hist[kb[i]], 1u)] = i;
+    } else {
+        for (uint32_t q0 = 0; q0 < nq; q0 += 4u * 256u) {
+            u32x4 v[4];
+            load_costs16(F.tile_cost, q0, nq, v);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t q = q0 + (uint32_t)u * 256u + tid;
+                if (q < nq) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) F.lpt_next[atomicAdd(&hist[lpt_key(v[u][j])], 1u)] = 4u * q + (uint32_t)j;
+                }
+            }
+        }
+        for (uint32_t i = 4u * nq + tid; i < nb; i += 256u) {
+            const uint32_t c = __hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            F.lpt_next[atomicAdd(&hist[lpt_key(c)], 1u)] = i;
+        }
+    }
+#else
     for (uint32_t i = tid; i < nb; i += 256) {
         const uint32_t c = __hip_atomic_load(F.tile_cost + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         F.lpt_next[atomicAdd(&hist[lpt_key(c)], 1u)] = i;
     }
+#endif
     if (tid == 0) __hip_atomic_store(F.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -843,6 +927,30 @@ struct rt_ctx {
 };
 
 static std::string g_err;
+
+// How the synchronous entry points (rt_render, rt_render_tiled: the reference's blocking
+// raytrace_gpgpu) wait for a frame.  hipStreamSynchronize may sleep until an interrupt; a frame
+// is a fraction of a millisecond, so they poll instead (hipStreamQuery, RTAMD_SYNC=query, the
+// default) for up to kSpinWaitMs and only then block.  RTAMD_SYNC=block: hipStreamSynchronize
+// at once (A/B).
+constexpr double kSpinWaitMs = 50.0;
+static int sync_mode() {
+    static const int m = [] {
+        const char* v = std::getenv("RTAMD_SYNC");
+        return v && std::strcmp(v, "block") == 0 ? 1 : 0;
+    }();
+    return m;
+}
+static hipError_t wait_stream(hipStream_t s) {
+    if (sync_mode() == 1) return hipStreamSynchronize(s);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return e;
+        if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > kSpinWaitMs)
+            return hipStreamSynchronize(s);
+    }
+}
 
 // frame counters (one parity set): 8 per bounce ([0] queue size, [2] the bounce launch's
 // work cursor), then the restart count (then, sized per frame, the queues' chunk sums)
@@ -1611,6 +1719,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.tile_cost = nullptr;
     F.lpt_next = nullptr;
     F.done = nullptr;
+    F.prio_blocks = 0;
     if (!(flags & RT_FLAG_STATIC_ORDER)) {
         const uint32_t units = F.num_blocks;
         const bool fresh = L.cost_cap < units || !L.d_done;
@@ -1627,7 +1736,10 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             L.cost_key = key;
             L.cost_ready = false;
         }
-        if (L.cost_ready) F.tile_order = L.d_lpt;
+        if (L.cost_ready) {
+            F.tile_order = L.d_lpt;
+            F.prio_blocks = std::min<uint32_t>(RTK_PRIO_BLOCKS, F.num_blocks);
+        }
         F.tile_cost = L.d_cost;
         F.lpt_next = L.d_lpt;
         F.done = L.d_done;
@@ -1637,7 +1749,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const bool fast = S.clean != 0 && !c->split_records;
     const dim3 grid(F.num_blocks), block(256);
     int ax = aux ? 1 : 0;
-    HIPC(c, hipEventRecord(E.e[0], s));
+    // A frame of one launch (depth 1, or the fused kernel) with RTK_EXT_EVENTS takes its timing
+    // events from the launch itself (hipExtLaunchKernel: start and stop stamped by the dispatch),
+    // instead of two marker packets around it on the stream.
+    const bool one_launch = (!wavefront || depth == 1) && !traced && !tline;
+    const bool ext_ev = RTK_EXT_EVENTS && one_launch;
+    if (!ext_ev) HIPC(c, hipEventRecord(E.e[0], s));
     (void)hipGetLastError();   // the launches below are checked with hipGetLastError: not an earlier call's error
 
     // The frame's first kernel zeroes the other parity set for the next frame: from then on
@@ -1645,7 +1762,8 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     // fails (its set's queue counts and cursors are then stale).
     if (!wavefront) {
         void* args[] = {&S, &F, &O, &ax};
-        HIPC(c, hipLaunchKernel(kernel_fused(math, fast), grid, block, args, 0, s));
+        if (ext_ev) HIPC(c, hipExtLaunchKernel(kernel_fused(math, fast), grid, block, args, 0, s, E.e[0], E.e[1], 0));
+        else HIPC(c, hipLaunchKernel(kernel_fused(math, fast), grid, block, args, 0, s));
         ++L.nframe;
     } else {
         // Wavefront: bounce 0 over tiles, then one persistent launch per further bounce
@@ -1685,6 +1803,8 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
                 if (!(O.wtime = tline_region(F.num_blocks * 4u)))
                     return set_err(c, "rt_wave_timeline: buffer too small", RT_ERR_INVALID_ARG);
                 HIPC(c, hipLaunchKernel(kernel_timeline_first(depth > 1), grid, block, args, 0, s));
+            } else if (ext_ev) {
+                HIPC(c, hipExtLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s, E.e[0], E.e[1], 0));
             } else {
                 HIPC(c, hipLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s));
             }
@@ -1726,7 +1846,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
         }
     }
     HIPC(c, hipGetLastError());
-    HIPC(c, hipEventRecord(E.e[1], s));
+    if (!ext_ev) HIPC(c, hipEventRecord(E.e[1], s));
     HIPC(c, hipEventRecord(L.idle, s));
     if (F.tile_cost) L.cost_ready = true;
     c->timing_valid = true;
@@ -1777,7 +1897,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         if (hipPointerGetAttributes(&pa, out_bgr) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer) {
             rc = rt_render_device(c, w, h, depth, flags, nullptr, (uint32_t*)pa.devicePointer, nullptr, c->stream);
             if (rc) return rc;
-            HIPC(c, hipStreamSynchronize(c->stream));
+            HIPC(c, wait_stream(c->stream));
             return RT_OK;
         }
         (void)hipGetLastError();   // pageable memory: not an error, the readback path below
@@ -1795,7 +1915,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
             if (aux->t) HIPC(c, hipMemcpyAsync(aux->t, c->d_t, npix * depth * 4, hipMemcpyDeviceToHost, c->stream));
             if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb, c->d_rgb, npix * 3 * 4, hipMemcpyDeviceToHost, c->stream));
         }
-        HIPC(c, hipStreamSynchronize(c->stream));
+        HIPC(c, wait_stream(c->stream));
         return RT_OK;
     }
     for (uint32_t g = 0; g < groups; ++g)   // group g's kernels and readback on gstream[g]
@@ -1842,7 +1962,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
             if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb + p0 * 3, c->d_rgb + p0 * 3, np * 3 * 4, hipMemcpyDeviceToHost, s));
         }
     }
-    for (uint32_t g = 0; g < groups; ++g) HIPC(c, hipStreamSynchronize(c->gstream[g]));
+    for (uint32_t g = 0; g < groups; ++g) HIPC(c, wait_stream(c->gstream[g]));
     c->last_group = slots;
     return RT_OK;
 }
@@ -2147,7 +2267,7 @@ int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t de
     // into the frame when this returns)
     for (int32_t k = 0; k < queued; ++k) {
         rt_ctx* c = ctxs[k];
-        const hipError_t e = hipSetDevice(c->device) == hipSuccess ? hipStreamSynchronize(c->stream) : hipErrorInvalidDevice;
+        const hipError_t e = hipSetDevice(c->device) == hipSuccess ? wait_stream(c->stream) : hipErrorInvalidDevice;
         if (e != hipSuccess && rc == RT_OK)
             rc = set_err(c0, "rt_render_tiled: ctxs[" + std::to_string(k) + "]: " + hipGetErrorString(e), RT_ERR_DEVICE);
     }

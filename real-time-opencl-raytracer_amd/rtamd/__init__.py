@@ -189,6 +189,8 @@ def lib() -> C.CDLL:
             "rt_camera_frame_params": (C.c_int, [vp, vp, u32, u32, vp, vp, C.POINTER(rt_params)]),
         }
         for name, (res, args) in sig.items():
+            if not hasattr(L, name):   # an older build loaded for an A/B (RTAMD_LIB): its own symbols only
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

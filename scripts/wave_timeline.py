@@ -102,6 +102,24 @@ def run_config(name, outdir, frames):
     res["launches"] = [summarize(rec) for rec in tl["launches"]]
     np.savez_compressed(os.path.join(outdir, f"timeline_{name}.npz"),
                         **{f"l{k}_{f}": v for k, rec in enumerate(tl["launches"]) for f, v in rec.items()})
+    # lone waves: the same scene and camera at 16x16 (one block: 4 waves on one CU) and 128x64
+    # (32 blocks): per-trip time of the traversal when a wave has its CU (almost) to itself
+    lone = {}
+    for lw, lh in ((16, 16), (128, 64)):
+        r.set_params(mesh.camera_params(lw, lh))
+        for _ in range(5):
+            r.render_device(lw, lh, depth, flags, dev.data_ptr())
+        torch.cuda.synchronize()
+        tl1 = r.wave_timeline(lw, lh, depth, flags)
+        rec = tl1["launches"][0]
+        trips = rec["main"] + rec["prologue"]
+        dur = (rec["t1"] - rec["t0"]) * 10.0   # ns
+        k = trips > 0
+        lone[f"{lw}x{lh}"] = {"waves": int(len(trips)), "frame_us": tl1["frame_ns"] / 1e3,
+                              "ns_per_trip": round(float(dur[k].sum() / trips[k].sum()), 1) if k.any() else None,
+                              "max_trips": int(trips.max()), "max_wave_us": round(float(dur.max()) / 1e3, 2)}
+    res["lone_waves"] = lone
+    r.set_params(p)
     # and the same frame with the static block order (RT_FLAG_STATIC_ORDER = 16)
     tls = r.wave_timeline(w, h, depth, flags | 16)
     res["static_order"] = {"frame_kernels_ms": tls["frame_ns"] / 1e6,

@@ -84,9 +84,9 @@ def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
     assert "rt_bands_put" in res["config"]["band_exchange"]
     fd, fc = res["config"]["frame_delivery"], res["config"]["frame_check"]
     assert fd["status"] == 0 and fd["frames_presented"] == fd["frames_rendered"] == 26
-    assert fc["presented_frames_checksummed"] == 26 and fc["checksum_mismatches"] == 0
-    assert fc["held_frames_checked"] == 8 and fc["distinct_cameras"] == 26
-    assert res["config"]["gathered_frame_equals_single_rank_render"] is True
+    assert fc["presented_frames_checksummed"] == 26 and fc["checksum_mismatches"] == 0, fc
+    assert fc["held_frames_checked"] == 8 and fc["distinct_cameras"] == 26, fc
+    assert res["config"]["gathered_frame_equals_single_rank_render"] is True, fc
     assert res["config"]["setup_skew_s"] is not None and res["config"]["band_exchange_fallback"] is None
     print(f"{n} ranks: set-up skew {res['config']['setup_skew_s']} s")
 
@@ -106,7 +106,8 @@ def test_a_late_rank_at_set_up(barrier):
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     cfg = res["config"]
     assert cfg["setup_skew_s"] >= 2.5, cfg["setup_skew_s"]
-    assert cfg["gathered_frame_equals_single_rank_render"] is True
+    assert cfg["gathered_frame_equals_single_rank_render"] is True, (cfg.get("frame_check"), cfg.get("frame_delivery"),
+                                                                     cfg["band_exchange_fallback"], _why(p))
     if barrier:
         assert cfg["band_exchange_fallback"] is None and "rt_bands_put" in cfg["band_exchange"]
         assert cfg["frame_delivery"]["status"] == 0

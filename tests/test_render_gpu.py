@@ -673,3 +673,33 @@ def test_render_readback_paths_agree(renderer):
         assert np.array_equal(a["hits"].reshape(-1), hits.cpu().numpy()), (depth, flags)
         assert np.array_equal(a["t"].reshape(-1).view(np.uint32), tt.cpu().numpy().view(np.uint32)), (depth, flags)
         assert np.array_equal(a["rgb"].reshape(-1).view(np.uint32), rgb.cpu().numpy().view(np.uint32)), (depth, flags)
+
+
+@pytest.mark.parametrize("w,h,depth,flags", [(640, 360, 1, 0), (1920, 1080, 1, 0), (3840, 2160, 1, 0),
+                                             (640, 360, 3, WAVEFRONT | WF_SORT)])
+def test_adaptive_order_renders_every_tile_of_a_moving_camera(renderer, w, h, depth, flags):
+    """Frames of an orbiting camera rendered one after another on one stream each use the
+    longest-first block order the previous frame's last block built (rtk::tile_epilogue: costs
+    read 16 per thread per round trip, bucket keys kept in LDS up to kKeyBytes blocks, re-read
+    beyond: 3840x2160 has 32,400 blocks).  Every frame starts from a sentinel-filled buffer and
+    must equal the static-order render of its camera: an order that is not a permutation of the
+    blocks leaves sentinel pixels (a skipped tile) behind."""
+    import torch
+    import rtamd
+    d = load_golden("knot16k")
+    renderer.upload(_scene(d))
+    m = rtamd.Mesh.torus_knot(128, 64)
+    cam = rtamd.Camera()
+    buf = torch.empty(w * h, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    for f in range(5):
+        cam.add_rotate(0.07, 0.0)
+        renderer.set_params(rtamd.params_to_array(cam.params(m, w, h)))
+        with torch.cuda.stream(s):
+            buf.fill_(-1)
+        renderer.render_device(w, h, depth, flags, buf.data_ptr(), stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy().view(np.uint32)
+        want = renderer.render(w, h, depth=depth, flags=flags | 16)   # RT_FLAG_STATIC_ORDER
+        bad = int(np.sum(got != want))
+        assert bad == 0, f"frame {f}: {bad} pixels differ ({int(np.sum(got == 0xFFFFFFFF))} sentinel)"
