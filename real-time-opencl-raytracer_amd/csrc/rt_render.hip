@@ -68,8 +68,8 @@
                             // around the launch (C2 0.0747 vs 0.0764 ms, rt_render into pageable memory 0.527
                             // vs 0.548 ms; C3, C5 equal: profiles/r05/ab/ext_events_ab.log)
 #endif
-#ifndef RTK_PRIO_BLOCKS
-#define RTK_PRIO_BLOCKS 0   // blocks at the head of the longest-first order that run at wave priority 2
+#ifndef RTK_SHADE_EXP
+#define RTK_SHADE_EXP 0     // A/B experiments on the shading fetch only (2: none; pixels wrong)
 #endif
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
@@ -117,7 +117,6 @@ struct Frame {
     uint32_t* done;               // blocks finished so far (the last one builds lpt_next)
     uint32_t* zero_next;          // the other parity's frame counters, zeroed by this frame
     uint32_t nzero;
-    uint32_t prio_blocks;         // the first prio_blocks blocks of a longest-first order run at raised wave priority
 };
 
 // A ray in flight between bounces: {pix, o.xyz}, {d.xyz, shadow_sum}, {colour.xyz, 3 * triangle it leaves from}.
@@ -1719,7 +1718,6 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.tile_cost = nullptr;
     F.lpt_next = nullptr;
     F.done = nullptr;
-    F.prio_blocks = 0;
     if (!(flags & RT_FLAG_STATIC_ORDER)) {
         const uint32_t units = F.num_blocks;
         const bool fresh = L.cost_cap < units || !L.d_done;
@@ -1736,10 +1734,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             L.cost_key = key;
             L.cost_ready = false;
         }
-        if (L.cost_ready) {
-            F.tile_order = L.d_lpt;
-            F.prio_blocks = std::min<uint32_t>(RTK_PRIO_BLOCKS, F.num_blocks);
-        }
+        if (L.cost_ready) F.tile_order = L.d_lpt;
         F.tile_cost = L.d_cost;
         F.lpt_next = L.d_lpt;
         F.done = L.d_done;

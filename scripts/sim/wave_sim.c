@@ -29,12 +29,13 @@ static f3 nrm(f3 a) { float l = sqrtf(dot(a, a)); return l > 0 ? mul(a, 1.0f / l
 typedef struct {
     f3 o, d;
     int stack[70]; int sc;   // stack[sc-1] = cur
+    float dist[70];          // CULL: entry distance of a pushed far child (-inf: unknown)
     int tk, tend;            // leaf state
     float th; int res; int any; int done;
 } lane;
 
 static void lane_init(lane* L, f3 o, f3 d, int any) {
-    L->o = o; L->d = nrm(d); L->sc = 1; L->stack[0] = 0; L->th = 4294967296.0f; L->res = -1; L->any = any; L->done = 0;
+    L->o = o; L->d = nrm(d); L->sc = 1; L->stack[0] = 0; L->dist[0] = -INFINITY; L->th = 4294967296.0f; L->res = -1; L->any = any; L->done = 0;
     L->tk = L->tend = 0;
     if (N[0].l < 0) { L->tk = N[0].off; L->tend = N[0].off + N[0].cnt; }
 }
@@ -55,6 +56,20 @@ static int lane_record(const lane* L) {
 static void enter_top(lane* L) {
     if (L->sc > 0) { int c = L->stack[L->sc - 1]; if (N[c].l < 0) { L->tk = N[c].off; L->tend = N[c].off + N[c].cnt; } }
 }
+static int CULL = 0;             // env CULL=1: a popped inner entry whose entry distance (from its push)
+                                 // is beyond tHit is skipped (every entry); CULL=2: only the last pushed one
+static long long culled = 0;
+// pops: skip inner entries whose box entry (computed when pushed) is beyond the current tHit:
+// their visit would cull both children (child boxes lie inside)
+static void cull_top(lane* L) {
+    if (!CULL || L->any) return;
+    while (L->sc > 0) {
+        const int top = L->sc - 1, c = L->stack[top];
+        if (N[c].l < 0 || !(L->dist[top] > L->th)) return;
+        L->sc--; culled++;
+        if (CULL == 2) { for (int k = 0; k < L->sc; ++k) L->dist[k] = -INFINITY; }   // LDS entries carry none
+    }
+}
 static int T2 = 0, TT2 = 0;   // TT2=1: two triangles of one leaf per iteration   // env T2=1: an inner step that descends into an inner child runs that child's step too
 static int descended;  // set by lane_step: this inner step moved cur to a child (push or advance)
 static void lane_step(lane* L) {
@@ -66,10 +81,12 @@ static void lane_step(lane* L) {
         slab(L, &N[n->l], &n0, &f0); slab(L, &N[n->r], &n1, &f1);
         int i0 = n0 <= f0 && f0 >= 0.001f && n0 <= L->th, i1 = n1 <= f1 && f1 >= 0.001f && n1 <= L->th;
         int a = n->l, b = n->r;
-        if (i0 && i1) { if (n0 > n1) { int t = a; a = b; b = t; } L->stack[L->sc - 1] = b; L->stack[L->sc++] = a; if (L->sc >= 65) { L->done = 1; L->sc = 0; return; } }
-        else if (i0) L->stack[L->sc - 1] = a;
-        else if (i1) L->stack[L->sc - 1] = b;
-        else L->sc--;
+        if (i0 && i1) { float fb = n0 > n1 ? n0 : n1; if (n0 > n1) { int t = a; a = b; b = t; }
+                        if (CULL == 2) for (int k = 0; k < L->sc - 1; ++k) L->dist[k] = -INFINITY;
+                        L->dist[L->sc - 1] = fb; L->stack[L->sc - 1] = b; L->dist[L->sc] = -INFINITY; L->stack[L->sc++] = a; if (L->sc >= 65) { L->done = 1; L->sc = 0; return; } }
+        else if (i0) { L->stack[L->sc - 1] = a; L->dist[L->sc - 1] = -INFINITY; }
+        else if (i1) { L->stack[L->sc - 1] = b; L->dist[L->sc - 1] = -INFINITY; }
+        else { L->sc--; cull_top(L); }
         descended = (i0 || i1) && L->sc > 0;
         enter_top(L);
     } else {
@@ -91,7 +108,7 @@ static void lane_step(lane* L) {
         }
         L->tk++;
         if (stop) L->sc = 0;
-        else if (L->tk >= L->tend) { L->sc--; enter_top(L); }
+        else if (L->tk >= L->tend) { L->sc--; cull_top(L); enter_top(L); }
     }
     if (L->sc == 0) L->done = 1;
 }
@@ -155,6 +172,7 @@ int main(int argc, char** argv) {
     const int shadow = argc > 1 ? atoi(argv[1]) : 1;   // 0: primary rays only (C2)
     T2 = getenv("T2") ? atoi(getenv("T2")) : 0;
     TT2 = getenv("TT2") ? atoi(getenv("TT2")) : 0;
+    CULL = getenv("CULL") ? atoi(getenv("CULL")) : 0;
     size_t s;
     N = (node*)rd("c3_nodes.bin", &s); NN = (int)(s / sizeof(node));
     V = (float*)rd("c3_vertices.bin", 0); IDX = (int32_t*)rd("c3_indices.bin", 0); REF = (int32_t*)rd("c3_tri_indices.bin", 0);
@@ -212,6 +230,7 @@ int main(int argc, char** argv) {
     printf("lane steps %lld: lane utilisation of the wave iterations %.3f\n", lane_steps,
            (double)lane_steps / (64.0 * (double)(iters + iters_pro)));
     if (T2 || TT2) printf("T2: second inner steps taken without a fetch: %lld\n", t2_second);
+    if (CULL) printf("CULL=%d: popped inner entries skipped %lld\n", CULL, culled);
     printf("iters %lld prologue %lld  lane fetches(vec) %lld  quad req %lld (inner %lld tri %lld) lanes/qreq %.3f\n",
            iters, iters_pro, lanes_vec, q_vec, q_vec_inner, q_vec_tri, (double)lanes_vec / q_vec);
     printf("  primary: %lld iterations + %lld prologue; shadow: %lld + %lld\n",
