@@ -334,17 +334,21 @@ int rt_chase_peak(rt_ctx* ctx, uint32_t table_records, uint32_t iters, uint32_t 
  * gives one wave per SIMD (a lone chain's iteration time on an otherwise idle chip). */
 int rt_chase_latency(rt_ctx* ctx, uint32_t table_records, uint32_t iters, uint32_t group, uint32_t blocks, float* ms,
                      uint64_t* waves);
-/* Where one frame's time goes (diagnostics): renders a frame (flags as rt_render, default
- * arithmetic; depth 1, or the wavefront path) on the ctx stream, after the frames already
- * rendered there (so with the adaptive block order the product uses), with a stamping
- * instantiation of the same kernels.  words[0] = launches L, words[1..L] = waves per launch,
- * words[9] / [10] = the frame's kernels / its first launch (HIP events, ns), then from word 16
- * 8 words per wave, launch after launch, waves in blockIdx * 4 + wave order: s_memrealtime
- * (100 MHz, low 32 bits) at the wave's start, at the end of its rays and at its end (after the
- * block epilogue: the longest-first order build in the frame's last block); its main-loop and
- * wave-uniform-prologue traversal trips; HW_REG_XCC_ID; HW_REG_HW_ID; the tile it rendered (first
- * launch) or the 64-ray groups it took (bounce launches).  *used_words = words written. */
-int rt_wave_timeline(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* words,
+/* Where a frame's time goes (diagnostics): renders `frames` (1..8) frames in flight, frame f on
+ * its own stream (flags as rt_render, default arithmetic; depth 1, or the wavefront path), with
+ * a stamping instantiation of the same kernels, after a few untimed rounds on the same streams
+ * (so with the adaptive block order the product uses).  words[0] = launches L (<= 32),
+ * words[1] = frames, words[2] / [3] = the first frame's kernels / its first launch (HIP events,
+ * ns); per launch i: words[8 + i] = its waves, words[40 + i] = its frame, words[72 + i] = its
+ * bounce (0 = the first launch); from word 128, 16 words per wave, launch after launch, waves in
+ * blockIdx * 4 + wave order: s_memrealtime (100 MHz, low 32 bits) at the wave's start, when its
+ * closest-hit traversal returned, when its shading was done, at the end of its rays and at its
+ * end (after the block epilogue: the longest-first order build in the frame's last block); its
+ * closest-hit main-loop and wave-uniform-prologue trips and the same two for its shadow rays;
+ * HW_REG_XCC_ID; HW_REG_HW_ID; the tile it rendered (first launch) or the 64-ray groups it took
+ * (bounce launches; trips summed over them, times of the last); 4 zero words.
+ * *used_words = words written. */
+int rt_wave_timeline(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, int32_t frames, uint32_t* words,
                      uint64_t cap_words, uint64_t* used_words);
 
 /* Traversals of the last frame that outgrew the fast kernel's LDS stack and

@@ -283,26 +283,34 @@ __device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
     return (band * (uint32_t)F.nranks + (uint32_t)F.rank) * (uint32_t)F.band_rows + rib;
 }
 
-// Diagnostic instantiation only (rt_wave_timeline, TR = 2): a wave's traversal loop trips,
-// counted by its first active lane in the wave's LDS words c[0] (main loop) and c[1]
-// (wave-uniform prologue).
+// Diagnostic instantiation only (rt_wave_timeline, TR = 2).  Each wave keeps kTlWords LDS words:
+// [0] / [1] closest-hit main-loop / wave-uniform-prologue trips, [2] / [3] the same for the shadow
+// (any-hit) traversal, [4] s_memrealtime when the closest-hit traversal returned, [5] when the
+// shading was done (the shadow traversal starts); trips counted and times taken by the wave's
+// first active lane.  (In a persistent bounce wave: trips over all its groups, times of its last.)
+constexpr uint32_t kTlWords = 8, kTlRecord = 16;
 __device__ __forceinline__ void timeline_step(uint32_t* c, int which) {
     if ((uint32_t)(threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) c[which] += 1u;
 }
-// ... and its record (8 words, wave w of the launch): s_memrealtime (100 MHz, low 32 bits) at
-// its start, at the end of its rays and now; the two trip counts; HW_REG_XCC_ID; HW_REG_HW_ID
-// (CU, SIMD, wave slot); a tag (the tile, or the bounce kernel's groups taken).  Stamps go to
-// their own buffer only; nothing the frame computes reads them.
+__device__ __forceinline__ void timeline_mark(uint32_t* c, int which) {
+    if ((uint32_t)(threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))
+        c[which] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+}
+// ... and its record (kTlRecord words, wave w of the launch): [0] s_memrealtime (100 MHz, low 32
+// bits) at its start, [1] closest hit done, [2] shading done, [3] end of its rays, [4] its end (after
+// the block epilogue); [5..8] the four trip counts; [9] HW_REG_XCC_ID; [10] HW_REG_HW_ID (CU, SIMD,
+// wave slot); [11] a tag (the tile, or the bounce kernel's 64-ray groups).  Stamps go to their own
+// buffer only; nothing the frame computes reads them.
 __device__ __forceinline__ void timeline_store(const Outputs& O, uint32_t w, uint32_t t0, uint32_t t1,
                                                const uint32_t* c, uint32_t tag) {
     const uint32_t t2 = (uint32_t)__builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63u) == 0) {
-        uint32_t* r = O.wtime + (size_t)w * 8;
-        const uint4 a = make_uint4(t0, t1, t2, c[0]);
-        const uint4 b = make_uint4(c[1], (uint32_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)),
-                                   (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)), tag);
-        reinterpret_cast<uint4*>(r)[0] = a;
-        reinterpret_cast<uint4*>(r)[1] = b;
+        uint4* r = reinterpret_cast<uint4*>(O.wtime + (size_t)w * kTlRecord);
+        r[0] = make_uint4(t0, c[4], c[5], t1);
+        r[1] = make_uint4(t2, c[0], c[1], c[2]);
+        r[2] = make_uint4(c[3], (uint32_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)),
+                          (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)), tag);
+        r[3] = make_uint4(0u, 0u, 0u, 0u);
     }
 }
 
@@ -913,7 +921,9 @@ struct rt_ctx {
         bool on = false;
         uint32_t* d_words = nullptr; size_t cap = 0;   // device buffer, words
         size_t limit = 0, used = 0;                    // words the caller takes, words written
-        std::vector<uint32_t> waves;                   // waves per launch of the frame
+        std::vector<uint32_t> waves;                   // waves per launch
+        std::vector<uint32_t> frame, bounce;           // per launch: its frame (of those in flight), its bounce
+        uint32_t cur_frame = 0;
     } tline;
     bool frame_rows = false;   // rt_render_tiled: d_out is the whole frame (rtk::Outputs::frame_rows)
     uint32_t* h_stage = nullptr; size_t stage_cap = 0;   // rt_render_tiled: pinned frame for pageable callers
@@ -1652,10 +1662,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const bool tline = c->tline.on;
     // rt_wave_timeline: launch k's wave records at the next free words of the device buffer
     auto tline_region = [&](uint32_t waves) -> uint32_t* {
-        if (c->tline.used + (size_t)waves * 8 > c->tline.limit) return nullptr;
+        if (c->tline.used + (size_t)waves * rtk::kTlRecord > c->tline.limit) return nullptr;
         uint32_t* p = c->tline.d_words + c->tline.used;
-        c->tline.used += (size_t)waves * 8;
+        c->tline.used += (size_t)waves * rtk::kTlRecord;
         c->tline.waves.push_back(waves);
+        c->tline.frame.push_back(c->tline.cur_frame);
+        c->tline.bounce.push_back((uint32_t)c->tline.waves.size() - 1u);   // fixed up by the caller below
         return p;
     };
 
@@ -2274,36 +2286,71 @@ int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t de
 
 // ---- diagnostics: where a frame's time goes ----
 
-int rt_wave_timeline(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* words,
+int rt_wave_timeline(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, int32_t frames, uint32_t* words,
                      uint64_t cap_words, uint64_t* used_words) {
-    if (!c || !words || !used_words || cap_words < 16 || w == 0 || h == 0 || depth < 1 || depth > RT_MAX_DEPTH)
+    constexpr uint32_t kHead = 128, kMaxLaunches = 32;
+    if (!c || !words || !used_words || cap_words < kHead || w == 0 || h == 0 || depth < 1 || depth > RT_MAX_DEPTH ||
+        frames < 1 || frames > 8 || (uint64_t)frames * (uint64_t)depth > kMaxLaunches)
         return set_err(c, "rt_wave_timeline: invalid argument", RT_ERR_INVALID_ARG);
     if ((flags & (RT_FLAG_STRICT_MATH | RT_FLAG_HW_MATH | RT_FLAG_EXACT_DIV)) || (depth > 1 && !(flags & RT_FLAG_WAVEFRONT)) ||
         !c->have_scene || !c->clean || c->split_records)
         return set_err(c, "rt_wave_timeline: the default arithmetic's fast kernels of a clean scene, depth 1 or the wavefront path",
                        RT_ERR_INVALID_ARG);
     HIPC(c, hipSetDevice(c->device));
-    int rc = ensure(c, c->d_out, c->out_cap, (size_t)w * h);
+    const size_t npix = (size_t)w * h;
+    int rc = ensure(c, c->d_out, c->out_cap, npix * (size_t)frames);
     if (rc) return rc;
     if ((rc = ensure(c, c->tline.d_words, c->tline.cap, (size_t)cap_words))) return rc;
+    // frame f in flight renders on stream f: the ctx stream, then the row-group streams (their own
+    // frame slots and longest-first orders); a few untimed rounds first, so every stream's order is
+    // built from its own previous frame, as for the frames the product keeps in flight
+    hipStream_t st[8];
+    st[0] = c->stream;
+    for (int32_t f = 1; f < frames; ++f) {
+        if (!c->gstream[f - 1]) HIPC(c, hipStreamCreateWithFlags(&c->gstream[f - 1], hipStreamNonBlocking));
+        st[f] = c->gstream[f - 1];
+    }
+    if (frames > 1) {
+        for (int r = 0; r < 3; ++r)
+            for (int32_t f = 0; f < frames; ++f)
+                if ((rc = rt_render_device(c, w, h, depth, flags, nullptr, c->d_out + (size_t)f * npix, nullptr, st[f])))
+                    return rc;
+        for (int32_t f = 0; f < frames; ++f) HIPC(c, hipStreamSynchronize(st[f]));
+    }
     HIPC(c, hipMemsetAsync(c->tline.d_words, 0, (size_t)cap_words * 4, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
     c->tline.on = true;
-    c->tline.limit = (size_t)cap_words - 16;
+    c->tline.limit = (size_t)cap_words - kHead;
     c->tline.used = 0;
     c->tline.waves.clear();
-    rc = rt_render_device(c, w, h, depth, flags, nullptr, c->d_out, nullptr, c->stream);
+    c->tline.frame.clear();
+    c->tline.bounce.clear();
+    const uint64_t f0 = c->frames;
+    for (int32_t f = 0; f < frames && rc == RT_OK; ++f) {
+        c->tline.cur_frame = (uint32_t)f;
+        const size_t first = c->tline.waves.size();
+        rc = rt_render_device(c, w, h, depth, flags, nullptr, c->d_out + (size_t)f * npix, nullptr, st[f]);
+        for (size_t i = first; i < c->tline.bounce.size(); ++i) c->tline.bounce[i] = (uint32_t)(i - first);
+    }
     c->tline.on = false;
+    for (int32_t f = 0; f < frames; ++f) HIPC(c, hipStreamSynchronize(st[f]));
     if (rc) return rc;
-    HIPC(c, hipStreamSynchronize(c->stream));
     float t = 0.0f, k = 0.0f;
-    if ((rc = frame_times(c, c->frames - 1, t, k))) return rc;
-    std::memset(words, 0, 16 * 4);
-    words[0] = (uint32_t)c->tline.waves.size();
-    for (size_t i = 0; i < c->tline.waves.size() && i < 8; ++i) words[1 + i] = c->tline.waves[i];
-    words[9] = (uint32_t)std::lround((double)t * 1e6);   // the frame's kernels, HIP events, ns
-    words[10] = (uint32_t)std::lround((double)k * 1e6);  // its first launch
-    HIPC(c, hipMemcpy(words + 16, c->tline.d_words, c->tline.used * 4, hipMemcpyDeviceToHost));
-    *used_words = 16 + c->tline.used;
+    if ((rc = frame_times(c, f0, t, k))) return rc;   // the first frame's kernels
+    const size_t L = c->tline.waves.size();
+    if (L > kMaxLaunches) return set_err(c, "rt_wave_timeline: too many launches", RT_ERR_INVALID_ARG);
+    std::memset(words, 0, kHead * 4);
+    words[0] = (uint32_t)L;
+    words[1] = (uint32_t)frames;
+    words[2] = (uint32_t)std::lround((double)t * 1e6);   // the first frame's kernels, HIP events, ns
+    words[3] = (uint32_t)std::lround((double)k * 1e6);   // its first launch
+    for (size_t i = 0; i < L; ++i) {
+        words[8 + i] = c->tline.waves[i];
+        words[40 + i] = c->tline.frame[i];
+        words[72 + i] = c->tline.bounce[i];
+    }
+    HIPC(c, hipMemcpy(words + kHead, c->tline.d_words, c->tline.used * 4, hipMemcpyDeviceToHost));
+    *used_words = kHead + c->tline.used;
     return RT_OK;
 }
 

@@ -155,7 +155,7 @@ def lib() -> C.CDLL:
             "rt_gather_peak": (C.c_int, [vp, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
             "rt_chase_peak": (C.c_int, [vp, u32, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
             "rt_chase_latency": (C.c_int, [vp, u32, u32, u32, u32, C.POINTER(f32), C.POINTER(C.c_uint64)]),
-            "rt_wave_timeline": (C.c_int, [vp, u32, u32, i32, u32, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
+            "rt_wave_timeline": (C.c_int, [vp, u32, u32, i32, u32, i32, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
             "rt_last_timing": (C.c_int, [vp, C.POINTER(f32), C.POINTER(f32)]),
             "rt_timing_average": (C.c_int, [vp, i32, C.POINTER(f32), C.POINTER(f32)]),
             "rt_last_deferred": (C.c_int, [vp, C.POINTER(u32)]),
@@ -496,28 +496,33 @@ class Renderer:
                self._h)
         return ms.value, waves.value
 
-    def wave_timeline(self, w: int, h: int, depth: int = 1, flags: int = 0, cap_words: int = 1 << 24):
-        """rt_wave_timeline: one frame with per-wave stamps.  Returns {"frame_ns", "first_ns", "launches":
-        [structured array per launch: t0, t1, t2 (10 ns ticks, relative to the frame's first wave
-        start), main, prologue (loop trips), xcc, hwid, tag]}."""
+    def wave_timeline(self, w: int, h: int, depth: int = 1, flags: int = 0, frames: int = 1, cap_words: int = 1 << 25):
+        """rt_wave_timeline: `frames` frames in flight with per-wave stamps.  Returns {"frame_ns",
+        "first_ns", "frames", "launches": [per launch {"frame", "bounce", and arrays t0, t_trace, t_shade,
+        t1, t2 (10 ns ticks relative to the earliest wave start of all launches, -1 = not stamped),
+        main, prologue (loop trips, both rays), main_c, pro_c, main_s, pro_s (closest-hit / shadow),
+        xcc, hwid, tag}]}."""
         buf = np.zeros(cap_words, np.uint32)
         used = C.c_uint64()
-        _check(lib().rt_wave_timeline(self._h, w, h, depth, flags, _ptr(buf), cap_words, C.byref(used)), self._h)
+        _check(lib().rt_wave_timeline(self._h, w, h, depth, flags, frames, _ptr(buf), cap_words, C.byref(used)),
+               self._h)
         nl = int(buf[0])
-        recs, off = [], 16
+        recs, off = [], 128
         for k in range(nl):
-            nw = int(buf[1 + k])
-            recs.append(buf[off:off + nw * 8].reshape(nw, 8).copy())
-            off += nw * 8
-        base = min(int(r[:, 0].min()) for r in recs) if recs else 0
+            nw = int(buf[8 + k])
+            recs.append((int(buf[40 + k]), int(buf[72 + k]), buf[off:off + nw * 16].reshape(nw, 16).copy()))
+            off += nw * 16
+        base = min(int(r[:, 0].min()) for _, _, r in recs) if recs else 0
         out = []
-        for r in recs:
+        for fr, bo, r in recs:
             a = r.astype(np.int64)
-            for j in range(3):   # 32-bit tick wrap: relative to the first start
-                a[:, j] = (r[:, j].astype(np.int64) - base) & 0xFFFFFFFF
-            out.append({"t0": a[:, 0], "t1": a[:, 1], "t2": a[:, 2], "main": a[:, 3], "prologue": a[:, 4],
-                        "xcc": a[:, 5] & 0xF, "hwid": a[:, 6], "tag": a[:, 7]})
-        return {"frame_ns": int(buf[9]), "first_ns": int(buf[10]), "launches": out}
+            for j in range(5):   # 32-bit tick wrap: relative to the first start (0 = not stamped)
+                a[:, j] = np.where(r[:, j] == 0, -1, (r[:, j].astype(np.int64) - base) & 0xFFFFFFFF)
+            out.append({"frame": fr, "bounce": bo, "t0": a[:, 0], "t_trace": a[:, 1], "t_shade": a[:, 2],
+                        "t1": a[:, 3], "t2": a[:, 4], "main": a[:, 5] + a[:, 7], "prologue": a[:, 6] + a[:, 8],
+                        "main_c": a[:, 5], "pro_c": a[:, 6], "main_s": a[:, 7], "pro_s": a[:, 8],
+                        "xcc": a[:, 9] & 0xF, "hwid": a[:, 10], "tag": a[:, 11]})
+        return {"frame_ns": int(buf[2]), "first_ns": int(buf[3]), "frames": int(buf[1]), "launches": out}
 
     def copy_scene_from(self, src: "Renderer") -> None:
         """rt_scene_copy: this ctx gets src's uploaded scene (device to device / peer to peer)."""

@@ -70,6 +70,7 @@ static void cull_top(lane* L) {
         if (CULL == 2) { for (int k = 0; k < L->sc; ++k) L->dist[k] = -INFINITY; }   // LDS entries carry none
     }
 }
+static long long deep_lanes = 0;   // lanes whose stack outgrew the LDS part (the product restarts them)
 static int T2 = 0, TT2 = 0;   // TT2=1: two triangles of one leaf per iteration   // env T2=1: an inner step that descends into an inner child runs that child's step too
 static int descended;  // set by lane_step: this inner step moved cur to a child (push or advance)
 static void lane_step(lane* L) {
@@ -83,7 +84,9 @@ static void lane_step(lane* L) {
         int a = n->l, b = n->r;
         if (i0 && i1) { float fb = n0 > n1 ? n0 : n1; if (n0 > n1) { int t = a; a = b; b = t; }
                         if (CULL == 2) for (int k = 0; k < L->sc - 1; ++k) L->dist[k] = -INFINITY;
-                        L->dist[L->sc - 1] = fb; L->stack[L->sc - 1] = b; L->dist[L->sc] = -INFINITY; L->stack[L->sc++] = a; if (L->sc >= 65) { L->done = 1; L->sc = 0; return; } }
+                        L->dist[L->sc - 1] = fb; L->stack[L->sc - 1] = b; L->dist[L->sc] = -INFINITY; L->stack[L->sc++] = a;
+                        if (L->sc - 2 == 16) deep_lanes++;   // kLdsStack = 16: the product restarts this ray
+                        if (L->sc >= 65) { L->done = 1; L->sc = 0; return; } }
         else if (i0) { L->stack[L->sc - 1] = a; L->dist[L->sc - 1] = -INFINITY; }
         else if (i1) { L->stack[L->sc - 1] = b; L->dist[L->sc - 1] = -INFINITY; }
         else { L->sc--; cull_top(L); }
@@ -231,6 +234,7 @@ int main(int argc, char** argv) {
            (double)lane_steps / (64.0 * (double)(iters + iters_pro)));
     if (T2 || TT2) printf("T2: second inner steps taken without a fetch: %lld\n", t2_second);
     if (CULL) printf("CULL=%d: popped inner entries skipped %lld\n", CULL, culled);
+    printf("rays whose stack outgrew 16 LDS entries: %lld\n", deep_lanes);
     printf("iters %lld prologue %lld  lane fetches(vec) %lld  quad req %lld (inner %lld tri %lld) lanes/qreq %.3f\n",
            iters, iters_pro, lanes_vec, q_vec, q_vec_inner, q_vec_tri, (double)lanes_vec / q_vec);
     printf("  primary: %lld iterations + %lld prologue; shadow: %lld + %lld\n",

@@ -62,6 +62,29 @@ def summarize(rec, us_per_tick=0.01):
                        for x in np.unique(rec["xcc"])},
         "xcc_waves": {int(x): int((rec["xcc"] == x).sum()) for x in np.unique(rec["xcc"])},
     }
+    # phases of a wave (first launch: its 64 rays; bounce launch: its last group): closest-hit
+    # traversal, shading, shadow traversal; durations, and least-squares cost per trip of each
+    # traversal (duration ~ a * main trips + b * prologue trips + c) over the waves of the launch
+    if "t_trace" in rec and rec.get("bounce", 0) == 0:
+        tt, ts = rec["t_trace"], rec["t_shade"]
+        ok = work & (tt >= 0)
+        sh = ok & (ts >= 0)
+        ph = {"closest_us": (tt - t0)[ok] * us_per_tick, "shade_us": (ts - tt)[sh] * us_per_tick,
+              "shadow_us": (t1 - ts)[sh] * us_per_tick}
+        out["phase_us"] = {k: {q: round(pct(v, q), 2) for q in (50, 90, 100)} for k, v in ph.items()}
+        out["phase_us_total"] = {k: round(float(v.sum()), 1) for k, v in ph.items()}
+
+        def fit(dur, m, p, mask):
+            if mask.sum() < 16:
+                return None
+            A = np.stack([m[mask], p[mask], np.ones(mask.sum())], 1).astype(np.float64)
+            coef = np.linalg.lstsq(A, dur[mask].astype(np.float64), rcond=None)[0]
+            return {"ns_per_main_trip": round(float(coef[0]) * 1e3, 1), "ns_per_prologue_trip": round(float(coef[1]) * 1e3, 1),
+                    "ns_fixed": round(float(coef[2]) * 1e3, 1)}
+        out["fit_closest"] = fit((tt - t0) * us_per_tick, rec["main_c"], rec["pro_c"], ok)
+        out["fit_shadow"] = fit((t1 - ts) * us_per_tick, rec["main_s"], rec["pro_s"], sh)
+    if "main_c" in rec:
+        out["trips_by_kind"] = {k: int(rec[k].sum()) for k in ("main_c", "pro_c", "main_s", "pro_s")}
     heavy = work & (trips >= 64)
     if heavy.any():
         per = dur[heavy] / trips[heavy] * 1e3
@@ -120,12 +143,37 @@ def run_config(name, outdir, frames):
                               "max_trips": int(trips.max()), "max_wave_us": round(float(dur.max()) / 1e3, 2)}
     res["lone_waves"] = lone
     r.set_params(p)
+    # four frames in flight, as bench.py times them
+    res["inflight4"] = inflight(r, w, h, depth, flags, 4)
     # and the same frame with the static block order (RT_FLAG_STATIC_ORDER = 16)
     tls = r.wave_timeline(w, h, depth, flags | 16)
     res["static_order"] = {"frame_kernels_ms": tls["frame_ns"] / 1e6,
                            "first_launch": summarize(tls["launches"][0])}
     r.close()
     return res
+
+
+def inflight(r, w, h, depth, flags, frames, slots=8192):
+    """`frames` frames in flight (one stream each, rt_wave_timeline): how the launches of the
+    frames share the chip over time -- live waves per launch kind in 20 steps of the span, the
+    mean waves per SIMD over the span (wave-time / span / SIMDs), and each frame's span."""
+    tl = r.wave_timeline(w, h, depth, flags, frames=frames)
+    L = tl["launches"]
+    t_lo = min(int(x["t0"].min()) for x in L)
+    t_hi = max(int(x["t2"].max()) for x in L)
+    edges = np.linspace(t_lo, t_hi, 21)
+    kinds = sorted({x["bounce"] for x in L})
+    live = {f"bounce{k}": [int(sum(((x["t0"] <= e) & (x["t2"] > e)).sum() for x in L if x["bounce"] == k))
+                           for e in edges[:-1]] for k in kinds}
+    wave_time = sum(float((x["t2"] - x["t0"]).sum()) for x in L)
+    span = t_hi - t_lo
+    frames_span = {}
+    for f in range(frames):
+        xs = [x for x in L if x["frame"] == f]
+        frames_span[f] = round((max(int(x["t2"].max()) for x in xs) - min(int(x["t0"].min()) for x in xs)) / 100.0, 1)
+    return {"frames": frames, "span_us": round(span / 100.0, 1), "us_per_frame": round(span / 100.0 / frames, 1),
+            "mean_waves_per_simd": round(wave_time / span / (slots / 8), 3),
+            "frame_span_us": frames_span, "live_waves_at_5pct_steps": live}
 
 
 def chase(outdir):

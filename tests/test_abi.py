@@ -89,6 +89,6 @@ def test_multi_gpu_and_diagnostic_entry_points_reject_bad_arguments_without_gpu(
     assert lib.rt_render_tiled(two, 2, 8, 8, 9, 0, po) == -1     # depth > RT_MAX_DEPTH
     assert lib.rt_scene_copy(None, None) == -1
     used = C.c_uint64()
-    assert lib.rt_wave_timeline(None, 8, 8, 1, 0, po, 64, C.byref(used)) == -1
+    assert lib.rt_wave_timeline(None, 8, 8, 1, 0, 1, po, 256, C.byref(used)) == -1
     ms, waves = C.c_float(), C.c_uint64()
     assert lib.rt_chase_latency(None, 16, 4, 4, 1, C.byref(ms), C.byref(waves)) == -1
