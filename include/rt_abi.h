@@ -346,7 +346,8 @@ int rt_chase_latency(rt_ctx* ctx, uint32_t table_records, uint32_t iters, uint32
  * end (after the block epilogue: the longest-first order build in the frame's last block); its
  * closest-hit main-loop and wave-uniform-prologue trips and the same two for its shadow rays;
  * HW_REG_XCC_ID; HW_REG_HW_ID; the tile it rendered (first launch) or the 64-ray groups it took
- * (bounce launches; trips summed over them, times of the last); 4 zero words.
+ * (bounce launches; trips summed over them, times of the last); s_memrealtime when the closest-hit
+ * traversal started and when its wave-uniform prologue ended; 2 zero words.
  * *used_words = words written. */
 int rt_wave_timeline(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, int32_t frames, uint32_t* words,
                      uint64_t cap_words, uint64_t* used_words);

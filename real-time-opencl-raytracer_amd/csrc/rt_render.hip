@@ -286,7 +286,8 @@ __device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
 // Diagnostic instantiation only (rt_wave_timeline, TR = 2).  Each wave keeps kTlWords LDS words:
 // [0] / [1] closest-hit main-loop / wave-uniform-prologue trips, [2] / [3] the same for the shadow
 // (any-hit) traversal, [4] s_memrealtime when the closest-hit traversal returned, [5] when the
-// shading was done (the shadow traversal starts); trips counted and times taken by the wave's
+// shading was done (the shadow traversal starts), [6] when the closest-hit traversal started,
+// [7] when its wave-uniform prologue ended; trips counted and times taken by the wave's
 // first active lane.  (In a persistent bounce wave: trips over all its groups, times of its last.)
 constexpr uint32_t kTlWords = 8, kTlRecord = 16;
 __device__ __forceinline__ void timeline_step(uint32_t* c, int which) {
@@ -299,7 +300,8 @@ __device__ __forceinline__ void timeline_mark(uint32_t* c, int which) {
 // ... and its record (kTlRecord words, wave w of the launch): [0] s_memrealtime (100 MHz, low 32
 // bits) at its start, [1] closest hit done, [2] shading done, [3] end of its rays, [4] its end (after
 // the block epilogue); [5..8] the four trip counts; [9] HW_REG_XCC_ID; [10] HW_REG_HW_ID (CU, SIMD,
-// wave slot); [11] a tag (the tile, or the bounce kernel's 64-ray groups).  Stamps go to their own
+// wave slot); [11] a tag (the tile, or the bounce kernel's 64-ray groups); [12] closest-hit traversal
+// start, [13] end of its prologue.  Stamps go to their own
 // buffer only; nothing the frame computes reads them.
 __device__ __forceinline__ void timeline_store(const Outputs& O, uint32_t w, uint32_t t0, uint32_t t1,
                                                const uint32_t* c, uint32_t tag) {
@@ -310,7 +312,7 @@ __device__ __forceinline__ void timeline_store(const Outputs& O, uint32_t w, uin
         r[1] = make_uint4(t2, c[0], c[1], c[2]);
         r[2] = make_uint4(c[3], (uint32_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)),
                           (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)), tag);
-        r[3] = make_uint4(0u, 0u, 0u, 0u);
+        r[3] = make_uint4(c[6], c[7], 0u, 0u);
     }
 }
 

@@ -516,12 +516,13 @@ class Renderer:
         out = []
         for fr, bo, r in recs:
             a = r.astype(np.int64)
-            for j in range(5):   # 32-bit tick wrap: relative to the first start (0 = not stamped)
+            for j in (0, 1, 2, 3, 4, 12, 13):   # 32-bit tick wrap: relative to the first start (0 = not stamped)
                 a[:, j] = np.where(r[:, j] == 0, -1, (r[:, j].astype(np.int64) - base) & 0xFFFFFFFF)
             out.append({"frame": fr, "bounce": bo, "t0": a[:, 0], "t_trace": a[:, 1], "t_shade": a[:, 2],
                         "t1": a[:, 3], "t2": a[:, 4], "main": a[:, 5] + a[:, 7], "prologue": a[:, 6] + a[:, 8],
                         "main_c": a[:, 5], "pro_c": a[:, 6], "main_s": a[:, 7], "pro_s": a[:, 8],
-                        "xcc": a[:, 9] & 0xF, "hwid": a[:, 10], "tag": a[:, 11]})
+                        "xcc": a[:, 9] & 0xF, "hwid": a[:, 10], "tag": a[:, 11], "t_enter": a[:, 12],
+                        "t_pro_end": a[:, 13]})
         return {"frame_ns": int(buf[2]), "first_ns": int(buf[3]), "frames": int(buf[1]), "launches": out}
 
     def copy_scene_from(self, src: "Renderer") -> None:

@@ -69,7 +69,10 @@ def summarize(rec, us_per_tick=0.01):
         tt, ts = rec["t_trace"], rec["t_shade"]
         ok = work & (tt >= 0)
         sh = ok & (ts >= 0)
-        ph = {"closest_us": (tt - t0)[ok] * us_per_tick, "shade_us": (ts - tt)[sh] * us_per_tick,
+        te, tp = rec["t_enter"], rec["t_pro_end"]
+        ph = {"setup_us": (te - t0)[ok] * us_per_tick, "prologue_us": (tp - te)[ok] * us_per_tick,
+              "main_loop_us": (tt - tp)[ok] * us_per_tick,
+              "closest_us": (tt - t0)[ok] * us_per_tick, "shade_us": (ts - tt)[sh] * us_per_tick,
               "shadow_us": (t1 - ts)[sh] * us_per_tick}
         out["phase_us"] = {k: {q: round(pct(v, q), 2) for q in (50, 90, 100)} for k, v in ph.items()}
         out["phase_us_total"] = {k: round(float(v.sum()), 1) for k, v in ph.items()}
