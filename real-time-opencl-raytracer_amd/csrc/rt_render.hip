@@ -71,6 +71,11 @@
 #ifndef RTK_SHADE_EXP
 #define RTK_SHADE_EXP 0     // A/B experiments on the shading fetch only (2: none; pixels wrong)
 #endif
+#ifndef RTK_FAST_ENTRY
+#define RTK_FAST_ENTRY 0    // 1: frame kernels' entry without vector loads (the block's tile through the
+                            // scalar cache, the block size a constant): wave set-up 6.4 vs 7.3 us, but C3 /
+                            // C5 equal and C2 0.0757 vs 0.0747 ms (profiles/r05/ab/fast_entry_ab.log)
+#endif
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
 #endif
@@ -85,6 +90,7 @@ constexpr uint32_t kCntEscape = 31u;
 constexpr int kLdsStack = RTK_LDS_STACK;
 constexpr int kGlobalStack = 64 - kLdsStack;         // slots kLdsStack..63
 constexpr uint32_t kBlockPx = 16;                    // a block = 2 x 2 tiles of 8 x 8 pixels
+constexpr uint32_t kBlockThreads = 256;              // every frame kernel's block: 4 waves, one tile each
 
 struct DevScene {
     const float4* __restrict__ wnodes;   // [n_inner][4]
@@ -316,7 +322,19 @@ __device__ __forceinline__ void timeline_store(const Outputs& O, uint32_t w, uin
     }
 }
 
-__device__ __forceinline__ uint32_t block_tile(const Frame& F) { return F.tile_order[blockIdx.x]; }
+// The block's tile.  A uniform address: read through the scalar cache (RTK_FAST_ENTRY), not as a
+// vector load that would queue behind the traversal requests of the waves already running on the
+// CU.  The table is never written while a launch that reads it runs, except by that launch's
+// last block (the next frame's longest-first order), after every block has read its entry; the
+// next launch starts with the scalar cache invalidated.
+__device__ __forceinline__ uint32_t block_tile(const Frame& F) {
+#if RTK_FAST_ENTRY
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    return *((cu32*)F.tile_order + blockIdx.x);
+#else
+    return F.tile_order[blockIdx.x];
+#endif
+}
 
 // Lane -> pixel inside a block's 16x16 pixels: wave w holds 8x8 tile (w % 2, w / 2), lanes
 // in Morton order.  The vector-memory path merges the requests of the four lanes of a quad
@@ -335,8 +353,13 @@ __device__ __forceinline__ void tile_pixel(const Frame& F, uint32_t tb, int wave
 // other one for frame f + 1 on the same stream (the kernels of f never touch it), so no
 // launch is spent on zeroing.
 __device__ __forceinline__ void zero_next_counters(const Frame& F) {
-    const uint32_t n = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < F.nzero; i += n) F.zero_next[i] = 0u;
+#if RTK_FAST_ENTRY
+    const uint32_t bd = kBlockThreads;   // blockDim.x is a load from the dispatch packet
+#else
+    const uint32_t bd = blockDim.x;
+#endif
+    const uint32_t n = gridDim.x * bd;
+    for (uint32_t i = blockIdx.x * bd + threadIdx.x; i < F.nzero; i += n) F.zero_next[i] = 0u;
 }
 
 // Append to the wave's own segment: the active lanes get the next slots of segment `seg`,
@@ -1756,7 +1779,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     // the fast kernels (any quotient domain: traverse_fast picks the variant) need a clean scene
     // whose records one buffer descriptor covers
     const bool fast = S.clean != 0 && !c->split_records;
-    const dim3 grid(F.num_blocks), block(256);
+    const dim3 grid(F.num_blocks), block(rtk::kBlockThreads);
     int ax = aux ? 1 : 0;
     // A frame of one launch (depth 1, or the fused kernel) with RTK_EXT_EVENTS takes its timing
     // events from the launch itself (hipExtLaunchKernel: start and stop stamped by the dispatch),
