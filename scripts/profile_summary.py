@@ -20,7 +20,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "first_bounce_kernel<true, false, false>"   # C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray, not traced)
+KERNEL = "first_bounce_kernel<true, false, 0>"   # C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray, the product instantiation TR = 0)
 
 
 def counter(d, name):
