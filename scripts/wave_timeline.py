@@ -156,6 +156,27 @@ def run_config(name, outdir, frames):
     return res
 
 
+def inflight_only(name, sizes):
+    import torch
+    import rtamd
+    from rtamd import configs
+    cfg = configs.CONFIGS[name]
+    mesh, bvh, _ = configs.make_scene(cfg, threads=16)
+    r = rtamd.Renderer(0)
+    r.upload(rtamd.Scene.from_mesh(mesh, bvh))
+    r.set_params(mesh.camera_params(cfg["w"], cfg["h"]))
+    w, h, depth, flags = cfg["w"], cfg["h"], cfg["depth"], cfg["flags"]
+    dev = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    for _ in range(5):
+        r.render_device(w, h, depth, flags, dev.data_ptr())
+    torch.cuda.synchronize()
+    res = {"config": name}
+    for k in sizes:
+        res[f"inflight{k}"] = inflight(r, w, h, depth, flags, k)
+    r.close()
+    return res
+
+
 def inflight(r, w, h, depth, flags, frames, slots=8192):
     """`frames` frames in flight (one stream each, rt_wave_timeline): how the launches of the
     frames share the chip over time -- live waves per launch kind in 20 steps of the span, the
@@ -174,8 +195,12 @@ def inflight(r, w, h, depth, flags, frames, slots=8192):
     for f in range(frames):
         xs = [x for x in L if x["frame"] == f]
         frames_span[f] = round((max(int(x["t2"].max()) for x in xs) - min(int(x["t0"].min()) for x in xs)) / 100.0, 1)
+    # the middle half of the span (frames overlapping, neither ramp nor drain of the burst)
+    m_lo, m_hi = t_lo + 0.25 * span, t_lo + 0.75 * span
+    mid_time = sum(float((np.minimum(x["t2"], m_hi) - np.maximum(x["t0"], m_lo)).clip(min=0).sum()) for x in L)
     return {"frames": frames, "span_us": round(span / 100.0, 1), "us_per_frame": round(span / 100.0 / frames, 1),
             "mean_waves_per_simd": round(wave_time / span / (slots / 8), 3),
+            "mean_waves_per_simd_mid_half": round(mid_time / (0.5 * span) / (slots / 8), 3),
             "frame_span_us": frames_span, "live_waves_at_5pct_steps": live}
 
 
@@ -199,8 +224,17 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c2", "c3", "c5"])
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--no-chase", action="store_true")
+    ap.add_argument("--inflight-only", type=int, nargs="*", default=None,
+                    help="only the frames-in-flight bursts, of these sizes (1..8)")
     a = ap.parse_args()
     os.makedirs(a.outdir, exist_ok=True)
+    if a.inflight_only:
+        for name in a.configs:
+            res = inflight_only(name, a.inflight_only)
+            with open(os.path.join(a.outdir, f"inflight_{name}.json"), "w") as f:
+                json.dump(res, f, indent=1)
+            print(json.dumps(res), flush=True)
+        return
     if not a.no_chase:
         c = chase(a.outdir)
         print(json.dumps({"chase": c}), flush=True)
