@@ -417,6 +417,9 @@ __device__ __forceinline__ uint32_t lpt_key(uint32_t c) {
 #ifndef RTK_LPT_VEC
 #define RTK_LPT_VEC 1
 #endif
+#ifndef RTK_EPI_NOWAIT
+#define RTK_EPI_NOWAIT 0   // 1: the cost store and the counter add in flight together (profiles/r05/ab/epi_nowait_ab.log: equal)
+#endif
 constexpr int kEpilogueWords = 8 + 256 + 2 * 256;   // wave times + flag, histogram, two scan rows
 static_assert(4 * kLdsStack * 64 >= kEpilogueWords, "tile_epilogue's scratch must fit the blocks' traversal stacks");
 constexpr uint32_t kKeyBytes = (4u * kLdsStack * 64u - (uint32_t)kEpilogueWords) * 4u;
@@ -443,7 +446,13 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
     if (tid == 0) {
         const uint32_t c = max(max(scratch[0], scratch[1]), max(scratch[2], scratch[3]));
         __hip_atomic_store(F.tile_cost + tb, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // RTK_EPI_NOWAIT: where the last block reads every cost exactly once (the keys kept in
+        // LDS), the add does not wait for the store: the store and the add are in flight together
+        // (one round trip per block instead of two), and a cost that lands after the last block
+        // read it leaves the previous frame's cost of that block in this sort -- a key of the
+        // schedule, never of a pixel: the order is a permutation of the blocks either way.
+        // Grids read twice (past kKeyBytes blocks) need every cost stable between the passes.
+        if (!RTK_EPI_NOWAIT || !RTK_LPT_VEC || F.num_blocks > kKeyBytes) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t prev = __hip_atomic_fetch_add(F.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         scratch[4] = prev + 1u == F.num_blocks ? 1u : 0u;
     }
