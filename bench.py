@@ -64,6 +64,10 @@ def parse_args(argv=None):
                          "the exchange's host cost is paid once per B frames")
     ap.add_argument("--local-batch", action="store_true",
                     help="diagnostic: batches of --gather-batch frames per stream at N = 1 too (no exchange)")
+    ap.add_argument("--frames-per-launch", type=int, default=0,
+                    help="render each batch of K frames (K <= 8) with ONE launch (rt_render_device_batch: the "
+                         "longest tiles of all K frames first; depth-1 configs only); the frames in flight are then "
+                         "--inflight launches of K frames each.  0 (default): 4 for depth-1 configs, else 1")
     ap.add_argument("--hang-timeout", type=float, default=600.0,
                     help="N > 1: a rank that has not finished this many seconds after joining the process group "
                          "exits with status 3 (a stuck collective ends the run instead of hanging it)")
@@ -371,6 +375,11 @@ def run(args, world, result_out=None):
     # once per B frames
     # (ipc: a frame's put is one copy issued right after its render, no batching)
     B = max(1, args.gather_batch) if ((use_dist and not ipc) or args.local_batch) else 1
+    FPL = args.frames_per_launch if args.frames_per_launch > 0 else (4 if depth == 1 else 1)
+    if FPL > 1:   # a batch = the frames of one rt_render_device_batch launch (and of one gather at N > 1)
+        if depth != 1 or FPL > rtamd.RT_MAX_BATCH:
+            raise SystemExit(f"bench.py: --frames-per-launch needs a depth-1 config and K <= {rtamd.RT_MAX_BATCH}")
+        B = FPL
     # buffer sets: batch i uses set i % NB.  At N > 1 the sets cycle 2F ways, so a batch never
     # renders into a set whose gather was issued less than F batches earlier: the gathers run
     # in issue order on one RCCL stream (the process group's, or the rt_comm's), and a render
@@ -546,6 +555,9 @@ def run(args, world, result_out=None):
     # the per-frame host path, with everything constant bound once: at N = 8 a frame is
     # ~0.05 ms of GPU time, so the host's enqueue per frame has to stay well under that
     launch = r.frame_launcher(w, h, depth, flags, tiling)
+    blaunch = r.batch_launcher(w, h, depth, flags, tiling) if FPL > 1 else None
+    bcams = (rtamd.rt_params * B)() if FPL > 1 else None
+    base_params = rtamd.array_to_params(ptab[0])
     sh = [st.cuda_stream for st in streams]
     out_ptr = [[o[s].data_ptr() for s in range(B)] for o in outs]
     outs_ptr = [o.data_ptr() for o in outs]
@@ -629,14 +641,19 @@ def run(args, world, result_out=None):
                 pending[j] = None
             elif native:                 # likewise, through the rt_comm's events
                 slot_wait(j, sh[k])
-        if orbit_params is not None:   # updateCamera (RayTracer.cpp:609-672) for this frame
-            set_params(hdl, orbit_params[n % len(orbit_params)])
-        launch(out_ptr[j][s], sh[k])
+        if FPL > 1:   # the batch's cameras; one launch renders them all when the batch is full
+            bcams[s] = orbit_params[n % len(orbit_params)] if orbit_params is not None else base_params
+        else:
+            if orbit_params is not None:   # updateCamera (RayTracer.cpp:609-672) for this frame
+                set_params(hdl, orbit_params[n % len(orbit_params)])
+            launch(out_ptr[j][s], sh[k])
         frame_of[j][s] = n
         s += 1
         if s < B:
             cur[1] = s
             return
+        if FPL > 1:
+            blaunch(bcams, B, out_ptr[j][0], cap, sh[k])
         if use_dist:
             exchange(j, k, B)
         else:
@@ -646,6 +663,10 @@ def run(args, world, result_out=None):
     def drain():
         """Send a part-filled batch as it is; the caller then synchronises the device."""
         b, s = cur
+        if s and FPL > 1:   # the part-filled batch's frames, in one launch of s frames
+            blaunch(bcams, s, out_ptr[b % NB][0], cap, sh[b % F])
+            if not use_dist:
+                filled[b % NB] = s
         if s and use_dist:
             exchange(b % NB, b % F, s)
         cur[0], cur[1] = b + (1 if s else 0), 0
@@ -746,6 +767,26 @@ def run(args, world, result_out=None):
     # records on the launch stream around each frame's kernels (ring of 64 frames)
     frame_ms_avg, kernel_ms_avg = r.timing_average(min(args.steps, 64))
 
+    # --frames-per-launch at N = 1 (untimed, before anything else renders into the buffer sets):
+    # every frame they hold, rendered by a batch launch, equals a single rt_render_device frame
+    # of its camera
+    batch_check = None
+    if FPL > 1 and not use_dist:
+        torch.cuda.synchronize(dev)
+        one = torch.zeros(cap, dtype=torch.int32, device=dev)
+        n_checked, batch_ok = 0, True
+        for j in range(NB):
+            for s_ in range(filled[j]):
+                if frame_of[j][s_] < 0:
+                    continue
+                r.set_params(ptab[frame_of[j][s_] % ptab.shape[0]])
+                r.render_device(w, h, depth, flags, one.data_ptr(), tiling=tiling, stream=streams[0].cuda_stream)
+                torch.cuda.synchronize(dev)
+                n_checked += 1
+                batch_ok = batch_ok and bool(torch.equal(one[:npx], outs[j][s_][:npx]))
+        r.set_params(ptab[0])
+        batch_check = {"frames_checked": n_checked, "equal_to_single_renders": batch_ok}
+
     total_frames = warmup_frames + args.steps
     # frame n was rendered with camera n % L (the orbit table wraps when the time-based
     # warm-up ran past it; a static camera has L = 1)
@@ -798,6 +839,7 @@ def run(args, world, result_out=None):
             frame_check["held_frames_differing"] = held_bad[:16]
             frame_ok = frame_ok and not bad
         r.set_params(ptab[0])
+
 
     # (untimed for `value`) the reference's own boundary: rt_render, synchronous, the frame
     # read back into host memory (raytrace_gpgpu: launch + clFinish + clEnqueueReadBuffer,
@@ -934,7 +976,8 @@ def run(args, world, result_out=None):
     alg_bytes = frame_rays * bpr + 4.0 * frame_px            # reference-layout bytes per frame
     wavefront = depth > 1 and (flags & 8)
     ns = {0: "rtk_ref", 64: "rtk_strict", 2: "rtk_hw"}[math_flags]
-    kname = (f"{ns}::first_bounce_kernel<true, {'true' if depth > 1 else 'false'}, 0>" if (depth == 1 or wavefront)
+    kname = (f"{ns}::first_bounce_batch_kernel<true>" if FPL > 1
+             else f"{ns}::first_bounce_kernel<true, {'true' if depth > 1 else 'false'}, 0>" if (depth == 1 or wavefront)
              else f"{ns}::render_kernel<true>")
     # ---- roofline.  The path is a gather of 48-56 B records; its time is set by
     # the vector-memory path (TA/TD), not HBM (nodes and triangles are re-read from L1/L2/Infinity
@@ -1013,6 +1056,7 @@ def run(args, world, result_out=None):
                 "roof": "HBM (no fetch counts for this run)"}
     roof.update({"hbm": hbm, "stream_copy_gbs": round(stream_copy_gbs, 1), "kernel_ms": round(kernel_ms_avg, 4),
                  "frame_kernels_ms": round(frame_ms_avg, 4), "launches_overlap": F > 1, "kernel": kname,
+                 "frames_per_launch": FPL,
                  "records_per_ray_oracle": round(rec_inner + rec_tri, 2)})
     # HBM traffic: PMC counters need rocprofv3, so they come from separate profiling runs of this
     # command (scripts/pmc_c3.sh); the newest round's file is used and labelled as such, with the
@@ -1022,7 +1066,8 @@ def run(args, world, result_out=None):
         try:
             pj = json.load(open(pmc_files[-1]))
             lib_now = rtamd.library_digest()
-            roof["traffic"] = pj.get("hbm_bytes_per_launch")
+            # per frame, like `achieved` (a launch of the batch kernel renders frames_per_launch frames)
+            roof["traffic"] = pj.get("hbm_bytes_per_frame", pj.get("hbm_bytes_per_launch"))
             if pj.get("occupancy"):   # achieved waves per SIMD of the same kernel (PMC, separate run)
                 roof["occupancy"] = dict(pj["occupancy"], file=os.path.relpath(pmc_files[-1], ROOT),
                                          stale=pj.get("library_digest") != rtamd.library_digest())
@@ -1064,7 +1109,8 @@ def run(args, world, result_out=None):
                                    else f"screen bands x{world} ("
                                         + ("library RCCL gather" if native else "IPC band put" if ipc else "RCCL gather")
                                         + ")"),
-                   "band_rows": args.band_rows, "frames_in_flight": F, "frames_per_gather": B, "buffer_sets": NB,
+                   "band_rows": args.band_rows, "frames_in_flight": F, "frames_per_gather": B,
+                   "frames_per_launch": FPL, "buffer_sets": NB,
                    "band_exchange": (None if not use_dist else "rt_frame_exchange (one library RCCL communicator, gather + assembly streams)" if native
                                      else "rt_bands_put: each rank's bands copied straight into rank 0's frame "
                                           "(HIP IPC mapping, no collective)" if ipc
@@ -1089,6 +1135,8 @@ def run(args, world, result_out=None):
     if frame_ok is not None:
         res["config"]["gathered_frame_equals_single_rank_render"] = frame_ok
         res["config"]["frame_check"] = frame_check
+    if batch_check is not None:
+        res["config"]["batch_check"] = batch_check
     if sync_info is not None:
         res["config"]["frame_delivery"] = dict(sync_info, protocol=(
             "rt_bands_put_sync + rt_frame_present: every rank publishes its rows of each frame with a system-scope "
@@ -1099,6 +1147,8 @@ def run(args, world, result_out=None):
     if frame_latency is not None:
         res["config"]["frame_latency"] = frame_latency
     print(json.dumps(res), file=result_out or sys.stdout, flush=True)
+    if batch_check is not None and not batch_check["equal_to_single_renders"]:
+        raise SystemExit("bench.py: a batch-launch frame differs from its single render")
     if use_dist:
         dist.barrier()
         for c in comms:

@@ -188,6 +188,21 @@ int rt_scene_copy(rt_ctx* dst, rt_ctx* src);
 int rt_render_device(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,
                      const rt_tiling* tiling, uint32_t* d_out, const rt_aux* d_aux, void* stream);
 
+#define RT_MAX_BATCH 8
+/* Throughput mode of rt_render_device: nframes (1..RT_MAX_BATCH) frames of one size, frame i
+ * with camera params[i] (updateCamera's Params, RayTracer.cpp:609-672; every params[i] must
+ * carry the same scene box), rendered by ONE launch into d_out + i * frame_stride (pixels,
+ * frame_stride >= the rank's pixels).  The reference renders one frame per raytrace_gpgpu
+ * (RayTracer.cpp:330-344); a caller that keeps several frames in flight -- a frame loop, a
+ * server -- gets the longest tiles of all of them scheduled first in one grid instead of on
+ * separate streams.  depth 1 only (primary + shadow ray, RT_FLAG_NO_SHADOW for
+ * primary only), no aux planes; every frame's pixels equal rt_render_device's for its camera.
+ * Asynchronous like rt_render_device; rt_last_timing is the launch (all nframes frames).
+ * The ctx's own params (rt_set_params) are neither read nor changed. */
+int rt_render_device_batch(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,
+                           const rt_tiling* tiling, const rt_params* params, int32_t nframes, uint32_t* d_out,
+                           uint64_t frame_stride, void* stream);
+
 /* Number of pixels a rank owns under `tiling` (size of its output buffer). */
 int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* tiling);
 

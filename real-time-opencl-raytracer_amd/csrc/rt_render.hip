@@ -205,6 +205,17 @@ struct Outputs {
     uint32_t* wtime;
 };
 
+// rt_render_device_batch: the cameras of a launch's frames, a kernel argument (read with uniform
+// loads by first_bounce_batch_kernel), and the pixels between two frames' outputs.
+constexpr int kMaxBatch = RT_MAX_BATCH;
+struct BatchCam {
+    float4 a, b, c, campos, light_pos;   // .w unused
+};
+struct BatchCams {
+    BatchCam cam[kMaxBatch];
+    uint64_t stride;
+};
+
 __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
     uint32_t c = (ref >> 26) & 31u;
     if (c == kCntEscape) {
@@ -452,16 +463,16 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
         // read it leaves the previous frame's cost of that block in this sort -- a key of the
         // schedule, never of a pixel: the order is a permutation of the blocks either way.
         // Grids read twice (past kKeyBytes blocks) need every cost stable between the passes.
-        if (!RTK_EPI_NOWAIT || !RTK_LPT_VEC || F.num_blocks > kKeyBytes) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!RTK_EPI_NOWAIT || !RTK_LPT_VEC || gridDim.x > kKeyBytes) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t prev = __hip_atomic_fetch_add(F.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        scratch[4] = prev + 1u == F.num_blocks ? 1u : 0u;
+        scratch[4] = prev + 1u == gridDim.x ? 1u : 0u;
     }
     __syncthreads();
     if (!scratch[4]) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     uint32_t* hist = scratch + 8;      // [256]
     uint32_t* scan = hist + 256;       // [2][256]
-    const uint32_t nb = F.num_blocks;
+    const uint32_t nb = gridDim.x;   // the order's entries: every block of the launch (all frames of a batch)
     hist[tid] = 0;
     __syncthreads();
 #if RTK_LPT_VEC
@@ -945,7 +956,7 @@ struct rt_ctx {
     // static block orders (column strips), one per block grid: the row groups of rt_render and
     // the contexts of rt_render_tiled may differ in grid, and a grid's table is never rewritten
     // while a frame may read it (no stream sync to switch grids)
-    struct OrderTab { uint32_t tx, ty; uint32_t* d; };
+    struct OrderTab { uint32_t tx, ty, k; uint32_t* d; };   // k: frames per launch (rt_render_device_batch)
     static constexpr size_t kMaxOrders = 16;
     std::vector<OrderTab> orders;
     uint32_t scene_gen = 0;                                   // bumped by every upload
@@ -1150,6 +1161,9 @@ template <int M> struct Kernels;
             return next ? (void*)NS::first_bounce_kernel<true, true, 1> : (void*)NS::first_bounce_kernel<true, false, 1>; \
         }                                                                                                  \
         static void* traced_bounce() { return (void*)NS::wf_bounce_kernel<true, 1>; }                     \
+        static void* batch(bool fast) {                                                                    \
+            return fast ? (void*)NS::first_bounce_batch_kernel<true> : (void*)NS::first_bounce_batch_kernel<false>; \
+        }                                                                                                  \
     };
 RTK_KERNELS(0, rtk_strict)
 RTK_KERNELS(1, rtk_hw)
@@ -1158,6 +1172,9 @@ RTK_KERNELS(2, rtk_ref)
 
 static void* kernel_first(int m, bool fast, bool next) {
     return m == 0 ? Kernels<0>::first(fast, next) : m == 1 ? Kernels<1>::first(fast, next) : Kernels<2>::first(fast, next);
+}
+static void* kernel_batch(int m, bool fast) {
+    return m == 0 ? Kernels<0>::batch(fast) : m == 1 ? Kernels<1>::batch(fast) : Kernels<2>::batch(fast);
 }
 static void* kernel_fused(int m, bool fast) {
     return m == 0 ? Kernels<0>::fused(fast) : m == 1 ? Kernels<1>::fused(fast) : Kernels<2>::fused(fast);
@@ -1620,18 +1637,35 @@ int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* t) {
     return rows * w;
 }
 
-int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_tiling* tiling,
-                     uint32_t* d_out, const rt_aux* d_aux, void* stream) {
+// rt_render_device, and (batch != null) rt_render_device_batch: nbatch depth-1 frames with the
+// cameras batch[0..nbatch-1] in one launch, frame i at d_out + i * bstride
+static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_tiling* tiling,
+                         uint32_t* d_out, const rt_aux* d_aux, void* stream, const rt_params* batch, int32_t nbatch,
+                         uint64_t bstride) {
     if (!c || !d_out || w == 0 || h == 0 || depth < 0 || depth > RT_MAX_DEPTH)
         return set_err(c, "rt_render_device: invalid argument", RT_ERR_INVALID_ARG);
+    if (batch) {
+        if (nbatch < 1 || nbatch > rtk::kMaxBatch)
+            return set_err(c, "rt_render_device_batch: nframes must be 1.." + std::to_string(rtk::kMaxBatch), RT_ERR_INVALID_ARG);
+        if (depth != 1) return set_err(c, "rt_render_device_batch: depth 1 only", RT_ERR_INVALID_ARG);
+        for (int32_t i = 1; i < nbatch; ++i)
+            if (std::memcmp(&batch[i].scene_aabb_min, &batch[0].scene_aabb_min, 2 * sizeof(rt_float4)) != 0)
+                return set_err(c, "rt_render_device_batch: the frames' scene boxes differ", RT_ERR_INVALID_ARG);
+        if (c->trace.on || c->tline.on)
+            return set_err(c, "rt_render_device_batch: not with rt_fetch_counts / rt_wave_timeline", RT_ERR_INVALID_ARG);
+    }
+    const uint32_t K = batch ? (uint32_t)nbatch : 1u;
     if ((flags & RT_FLAG_STRICT_MATH) && (flags & RT_FLAG_HW_MATH))
         return set_err(c, "rt_render_device: RT_FLAG_STRICT_MATH and RT_FLAG_HW_MATH exclude each other", RT_ERR_INVALID_ARG);
     if (!c->have_scene) return set_err(c, "rt_render_device: no scene uploaded", RT_ERR_NO_SCENE);
-    if (!c->have_params) return set_err(c, "rt_render_device: no params set", RT_ERR_NO_SCENE);
+    if (!batch && !c->have_params) return set_err(c, "rt_render_device: no params set", RT_ERR_NO_SCENE);
     rt_tiling whole{0, 1, 16, 0};
     const rt_tiling* T = tiling ? tiling : &whole;
     const int64_t npix = rt_tiling_pixels(w, h, T);
     if (npix < 0) return set_err(c, "rt_render_device: bad tiling", RT_ERR_INVALID_ARG);
+    if (batch && bstride < (uint64_t)npix)
+        return set_err(c, "rt_render_device_batch: frame_stride below the frame's pixels", RT_ERR_INVALID_ARG);
+    if (batch && d_aux) return set_err(c, "rt_render_device_batch: no aux planes", RT_ERR_INVALID_ARG);
     const bool aux = d_aux && d_aux->hits && d_aux->t && d_aux->rgb;
     if (d_aux && !aux && (d_aux->hits || d_aux->t || d_aux->rgb))
         return set_err(c, "rt_render_device: aux needs hits, t and rgb together", RT_ERR_INVALID_ARG);
@@ -1652,7 +1686,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     const int math = (flags & RT_FLAG_STRICT_MATH) ? 0 : (flags & RT_FLAG_HW_MATH) ? 1 : 2;
 
     rtk::Frame F;
-    const rt_params& P = c->params;
+    const rt_params& P = batch ? batch[0] : c->params;
     F.a = make_float3(P.a.x, P.a.y, P.a.z);
     F.b = make_float3(P.b.x, P.b.y, P.b.z);
     F.c = make_float3(P.c.x, P.c.y, P.c.z);
@@ -1690,7 +1724,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     O.overflow = c->d_overflow;
     O.local_pixels = (uint64_t)npix;
     O.fcount = nullptr;
-    O.frame_rows = c->frame_rows ? 1u : 0u;
+    O.frame_rows = c->frame_rows && !batch ? 1u : 0u;
     O.wtime = nullptr;
     const bool traced = c->trace.on;
     const bool tline = c->tline.on;
@@ -1713,7 +1747,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     // the fused kernel specialised to a single bounce
     const bool wavefront = ((flags & RT_FLAG_WAVEFRONT) && depth > 0) || depth == 1;
 
-    if ((rc = ensure(c, L.d_gstack, L.gstack_cap, (size_t)npix * rtk::kGlobalStack))) return rc;
+    if ((rc = ensure(c, L.d_gstack, L.gstack_cap, (size_t)npix * rtk::kGlobalStack * K))) return rc;
     O.gstack = L.d_gstack;
     // frame counters, two parity sets: per bounce k (kBounceWords from kBounceWords k) its
     // queue size and its work cursor; [kRestartSlot] restarted traversals; then per queue
@@ -1738,7 +1772,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     // a new allocation, so frames in flight that read another grid's table never wait)
     F.tile_order = nullptr;
     for (const auto& o : c->orders)
-        if (o.tx == F.tiles_x && o.ty == F.tiles_y) F.tile_order = o.d;
+        if (o.tx == F.tiles_x && o.ty == F.tiles_y && o.k == K) F.tile_order = o.d;
     if (!F.tile_order) {
         if (c->orders.size() >= rt_ctx::kMaxOrders) {   // many grids: drop them all, once every frame is done
             HIPC(c, hipStreamSynchronize(s));
@@ -1747,7 +1781,12 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             for (auto& o : c->orders) (void)hipFree(o.d);
             c->orders.clear();
         }
-        const std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y);
+        std::vector<uint32_t> tab = tile_order_table(F.tiles_x, F.tiles_y);
+        if (K > 1) {   // a batch: each tile of the static order for every frame, side by side
+            std::vector<uint32_t> tk((size_t)tab.size() * K);
+            for (size_t i = 0; i < tk.size(); ++i) tk[i] = tab[i / K] + (uint32_t)(i % K) * F.num_blocks;
+            tab.swap(tk);
+        }
         uint32_t* d = nullptr;
         size_t cap = 0;
         if ((rc = ensure(c, d, cap, tab.size()))) return rc;
@@ -1756,7 +1795,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             (void)hipFree(d);
             return set_err(c, std::string("rt_render_device: order table: ") + hipGetErrorString(e), RT_ERR_DEVICE);
         }
-        c->orders.push_back(rt_ctx::OrderTab{F.tiles_x, F.tiles_y, d});
+        c->orders.push_back(rt_ctx::OrderTab{F.tiles_x, F.tiles_y, K, d});
         F.tile_order = d;
     }
     // Adaptive longest-first order from the previous frame of the same geometry on this
@@ -1765,7 +1804,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     F.lpt_next = nullptr;
     F.done = nullptr;
     if (!(flags & RT_FLAG_STATIC_ORDER)) {
-        const uint32_t units = F.num_blocks;
+        const uint32_t units = F.num_blocks * K;   // every frame's blocks (the order's entries)
         const bool fresh = L.cost_cap < units || !L.d_done;
         if ((rc = ensure(c, L.d_cost, L.cost_cap, units))) return rc;
         if ((rc = ensure(c, L.d_lpt, L.lpt_cap, units))) return rc;
@@ -1774,7 +1813,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
             if ((rc = ensure(c, L.d_done, one, 1))) return rc;
         }
         const uint64_t key = ((uint64_t)F.tiles_x << 48) ^ ((uint64_t)F.tiles_y << 32) ^ F.local_rows ^
-                             ((uint64_t)c->scene_gen << 20);
+                             ((uint64_t)c->scene_gen << 20) ^ ((uint64_t)K << 60);
         if (fresh || key != L.cost_key) {
             HIPC(c, hipMemsetAsync(L.d_done, 0, sizeof(uint32_t), s));
             L.cost_key = key;
@@ -1788,7 +1827,7 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     // the fast kernels (any quotient domain: traverse_fast picks the variant) need a clean scene
     // whose records one buffer descriptor covers
     const bool fast = S.clean != 0 && !c->split_records;
-    const dim3 grid(F.num_blocks), block(rtk::kBlockThreads);
+    const dim3 grid(F.num_blocks * K), block(rtk::kBlockThreads);
     int ax = aux ? 1 : 0;
     // A frame of one launch (depth 1, or the fused kernel) with RTK_EXT_EVENTS takes its timing
     // events from the launch itself (hipExtLaunchKernel: start and stop stamped by the dispatch),
@@ -1844,6 +1883,19 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
                 if (!(O.wtime = tline_region(F.num_blocks * 4u)))
                     return set_err(c, "rt_wave_timeline: buffer too small", RT_ERR_INVALID_ARG);
                 HIPC(c, hipLaunchKernel(kernel_timeline_first(depth > 1), grid, block, args, 0, s));
+            } else if (batch) {
+                rtk::BatchCams C{};
+                for (uint32_t i = 0; i < K; ++i) {
+                    const rt_params& Q = batch[i];
+                    C.cam[i] = rtk::BatchCam{make_float4(Q.a.x, Q.a.y, Q.a.z, 0.0f), make_float4(Q.b.x, Q.b.y, Q.b.z, 0.0f),
+                                             make_float4(Q.c.x, Q.c.y, Q.c.z, 0.0f),
+                                             make_float4(Q.campos.x, Q.campos.y, Q.campos.z, 0.0f),
+                                             make_float4(Q.light_pos.x, Q.light_pos.y, Q.light_pos.z, 0.0f)};
+                }
+                C.stride = bstride;
+                void* bargs[] = {&S, &F, &O, &C};
+                if (ext_ev) HIPC(c, hipExtLaunchKernel(kernel_batch(math, fast), grid, block, bargs, 0, s, E.e[0], E.e[1], 0));
+                else HIPC(c, hipLaunchKernel(kernel_batch(math, fast), grid, block, bargs, 0, s));
             } else if (ext_ev) {
                 HIPC(c, hipExtLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s, E.e[0], E.e[1], 0));
             } else {
@@ -1893,6 +1945,18 @@ int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     c->timing_valid = true;
     ++c->frames;
     return RT_OK;
+}
+
+int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_tiling* tiling,
+                     uint32_t* d_out, const rt_aux* d_aux, void* stream) {
+    return render_frames(c, w, h, depth, flags, tiling, d_out, d_aux, stream, nullptr, 1, 0);
+}
+
+int rt_render_device_batch(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_tiling* tiling,
+                           const rt_params* params, int32_t nframes, uint32_t* d_out, uint64_t frame_stride,
+                           void* stream) {
+    if (!params) return set_err(c, "rt_render_device_batch: no params", RT_ERR_INVALID_ARG);
+    return render_frames(c, w, h, depth, flags, tiling, d_out, nullptr, stream, params, nframes, frame_stride);
 }
 
 // rt_render: the reference's synchronous boundary (raytrace_gpgpu renders the whole frame, then

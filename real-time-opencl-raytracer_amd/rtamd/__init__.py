@@ -35,6 +35,7 @@ RT_FLAG_WAVEFRONT = 8
 RT_FLAG_WF_SORT = 32
 RT_FLAG_STRICT_MATH = 64
 RT_MAX_DEPTH = 8
+RT_MAX_BATCH = 8   # rt_render_device_batch frames per launch
 ERRORS = {0: "RT_OK", -1: "RT_ERR_INVALID_ARG", -2: "RT_ERR_DEVICE", -3: "RT_ERR_NO_SCENE",
           -4: "RT_ERR_OUT_OF_MEMORY", -5: "RT_ERR_BAD_SCENE"}
 
@@ -81,7 +82,7 @@ class rt_bvh_view(C.Structure):
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
 ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_tiled", "rt_scene_copy",
-               "rt_render_device",
+               "rt_render_device", "rt_render_device_batch",
                "rt_tiling_pixels", "rt_assemble_bands", "rt_assemble_bands_batch", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
                "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
                "rt_frame_ready_wait", "rt_ipc_export", "rt_ipc_open", "rt_ipc_close", "rt_bands_put",
@@ -123,6 +124,8 @@ def lib() -> C.CDLL:
             "rt_render_tiled": (C.c_int, [C.POINTER(vp), i32, u32, u32, i32, u32, vp]),
             "rt_scene_copy": (C.c_int, [vp, vp]),
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
+            "rt_render_device_batch": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), C.POINTER(rt_params), i32,
+                                                 vp, C.c_uint64, vp]),
             "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
             "rt_assemble_bands": (C.c_int, [vp, vp, C.c_uint64, u32, u32, i32, i32, vp]),
             "rt_assemble_bands_batch": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, i32, u32, u32, i32, i32, vp]),
@@ -569,6 +572,32 @@ class Renderer:
         ax = None if aux_ptrs is None else C.byref(rt_aux(*aux_ptrs))
         _check(lib().rt_render_device(self._h, w, h, depth, flags, None if tiling is None else C.byref(tiling),
                                       C.c_void_p(d_out_ptr), ax, C.c_void_p(stream or None)), self._h)
+
+    def render_device_batch(self, w, h, depth, flags, params, d_out_ptr: int, frame_stride: int,
+                            tiling: Optional[rt_tiling] = None, stream: Optional[int] = None):
+        """rt_render_device_batch: len(params) frames (rt_params, or the 32-float arrays of
+        params_to_array) in ONE launch, frame i with params[i] into d_out_ptr + 4 * i * frame_stride."""
+        _stream_arg(stream)
+        arr = (rt_params * max(1, len(params)))()
+        for i, p in enumerate(params):
+            arr[i] = p if isinstance(p, rt_params) else array_to_params(p)
+        _check(lib().rt_render_device_batch(self._h, w, h, depth, flags, None if tiling is None else C.byref(tiling),
+                                            arr, len(params), C.c_void_p(d_out_ptr), frame_stride,
+                                            C.c_void_p(stream or None)), self._h)
+
+    def batch_launcher(self, w, h, depth, flags, tiling: Optional[rt_tiling] = None):
+        """A callable (params_array, n, d_out_ptr, frame_stride, stream) -> None that enqueues n frames
+        like render_device_batch; params_array is a ctypes (rt_params * >= n) array the caller fills."""
+        fn = lib().rt_render_device_batch
+        hdl, tl = self._h, (None if tiling is None else C.byref(tiling))
+        w, h, depth, flags = C.c_uint32(w), C.c_uint32(h), C.c_int32(depth), C.c_uint32(flags)
+
+        def launch(arr, n: int, d_out_ptr: int, frame_stride: int, stream: int) -> None:
+            _stream_arg(stream)
+            rc = fn(hdl, w, h, depth, flags, tl, arr, n, d_out_ptr, frame_stride, stream)
+            if rc:
+                _check(rc, hdl)
+        return launch
 
     def frame_launcher(self, w, h, depth, flags, tiling: Optional[rt_tiling] = None):
         """A callable (d_out_ptr, stream) -> None that enqueues one frame like render_device,

@@ -26,7 +26,7 @@ for c in $cfgs; do
         python3 bench.py --config $c --steps 5 --warmup 1 --warmup-seconds 0 --no-cpu-baseline --no-roofline \
         --inflight 1 "$@" > $out/$c/p$i.log 2>&1 || { echo "$c pass $i ($set) failed"; exit 1; }
   done
-  for k in first_bounce_kernel wf_bounce_kernel wf_compact_sort_kernel; do
+  for k in first_bounce_kernel first_bounce_batch_kernel wf_bounce_kernel wf_compact_sort_kernel; do
     if grep -qs "$k" $out/$c/p1/*/*counter_collection.csv $out/$c/p1/*counter_collection.csv 2>/dev/null || \
        grep -rqs "$k" $out/$c/p1; then
       python3 scripts/pmc_summary.py --kernel $k --json $out/${c}_${k}.json $out/$c/p* > $out/${c}_${k}.txt

@@ -6,7 +6,7 @@ MI355X_MICROARCH.md HBM section); FETCH_SIZE / WRITE_SIZE are in kB = 1024 B.
 
     python scripts/profile_summary.py r02 [c3] [--occupancy PMC_JSON]
 
---occupancy: a per-kernel summary of scripts/pmc_configs.sh (MeanOccupancyPerCU pass of the
+--occupancy: a per-kernel summary of scripts/pmc_configs.sh, or its output directory (MeanOccupancyPerCU pass of the
 same kernel, one frame in flight): its achieved waves per SIMD go into pmc_<config>.json, which
 bench.py reports in roofline.occupancy.
 """
@@ -20,7 +20,11 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "first_bounce_kernel<true, false, 0>"   # C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray, the product instantiation TR = 0)
+# C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray, the product instantiation TR = 0),
+# or with bench.py's frames per launch > 1 (the depth-1 default) its batch form
+KERNEL_ONE = "first_bounce_kernel<true, false, 0>"
+KERNEL_BATCH = "first_bounce_batch_kernel<true>"
+KERNEL = KERNEL_ONE
 
 
 def counter(d, name):
@@ -32,13 +36,25 @@ def counter(d, name):
 
 def main():
     args = sys.argv[1:]
-    occ = None
+    occ_path = None
     if "--occupancy" in args:
         i = args.index("--occupancy")
-        occ = json.load(open(args[i + 1]))
+        occ_path = args[i + 1]
         args = args[:i] + args[i + 2:]
     rnd = args[0] if len(args) > 0 else "r01"
     cfg = args[1] if len(args) > 1 else "c3"
+    global KERNEL
+    tlog = os.path.join(ROOT, "gpurun_out", "prof_trace.log")
+    fpl = 1
+    if os.path.exists(tlog):
+        j = json.loads([ln for ln in open(tlog) if ln.startswith("{")][-1])
+        fpl = int(j["config"].get("frames_per_launch", 1))
+    KERNEL = KERNEL_BATCH if fpl > 1 else KERNEL_ONE
+    occ = None
+    if occ_path:   # a summary file, or scripts/pmc_configs.sh's output directory (the bench kernel's file in it)
+        if os.path.isdir(occ_path):
+            occ_path = os.path.join(occ_path, f"{cfg}_{KERNEL.split('<')[0]}.json")
+        occ = json.load(open(occ_path))
     out = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(out, exist_ok=True)
     stats = glob.glob(os.path.join(ROOT, "gpurun_out", "prof_trace", "**", "*kernel_stats.csv"), recursive=True)[0]
@@ -52,14 +68,15 @@ def main():
     # average bench.py printed for the same K frames
     timed_us = hip_ms = None
     trace = glob.glob(os.path.join(ROOT, "gpurun_out", "prof_trace", "**", "*kernel_trace.csv"), recursive=True)
-    tlog = os.path.join(ROOT, "gpurun_out", "prof_trace.log")
     if trace and os.path.exists(tlog):
-        j = json.loads([ln for ln in open(tlog) if ln.startswith("{")][-1])
         rows = sorted((r for r in csv.DictReader(open(trace[0])) if KERNEL in r["Kernel_Name"]),
                       key=lambda r: int(r["Start_Timestamp"]))
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
         wf = j.get("warmup_frames_run", j["warmup"])   # bench.py's time-based warm-up runs more frames
-        t = d[1 + wf: 1 + wf + j["steps"]]
+        if fpl > 1:   # only the warm-up and timed frames use the batch kernel: the timed launches are the last
+            t = d[-(j["steps"] // fpl):]
+        else:
+            t = d[1 + wf: 1 + wf + j["steps"]]
         timed_us = round(sum(t) / len(t), 2) if t else None
         hip_ms = j["roofline"]["kernel_ms"]
     fetch, nf, ff = counter("prof_fetch", "FETCH_SIZE")
@@ -81,6 +98,8 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 reports half the bytes of 16B/lane reads, MI355X_MICROARCH.md HBM); "
                       "kB = 1024 B",
         "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
+        "frames_per_launch": fpl,
+        "hbm_bytes_per_frame": int(round((2 * fetch + write) * 1024 / fpl)),
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --config " + cfg,
         # the library these passes ran (the profiled tree's lib/librtamd.so; bench.py marks the
         # traffic stale when it loads a different one)
@@ -95,7 +114,8 @@ def main():
             "kernel": occ["kernel"],
             "source": "rocprofv3 --pmc MeanOccupancyPerCU (SQ_LEVEL_WAVES accumulated over GRBM_GUI_ACTIVE per CU, "
                       "rocprofiler-sdk counter_defs.yaml for gfx950) / 4 SIMDs; counters are collected per dispatch, "
-                      "so this is one frame's kernel alone, ramp-up and tail included (scripts/pmc_configs.sh)"}
+                      "so this is one launch alone (frames_per_launch frames), ramp-up and tail included "
+                      "(scripts/pmc_configs.sh)"}
     json.dump(res, open(os.path.join(out, f"pmc_{cfg}.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 

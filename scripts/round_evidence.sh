@@ -22,7 +22,7 @@ export rnd
 scripts/gpu_steps.sh \
   "pytest_gpu|420|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" \
   "smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "profile|600|scripts/profile_c3.sh && PMC_SETS=occ scripts/pmc_configs.sh gpurun_out/$rnd/pmc_occ c3 && python scripts/profile_summary.py $rnd c3 --occupancy gpurun_out/$rnd/pmc_occ/c3_first_bounce_kernel.json && mkdir -p gpurun_out/profiles_$rnd && cp profiles/$rnd/c3_* profiles/$rnd/pmc_c3.json gpurun_out/profiles_$rnd/" \
+  "profile|600|scripts/profile_c3.sh && PMC_SETS=occ scripts/pmc_configs.sh gpurun_out/$rnd/pmc_occ c3 && python scripts/profile_summary.py $rnd c3 --occupancy gpurun_out/$rnd/pmc_occ && mkdir -p gpurun_out/profiles_$rnd && cp profiles/$rnd/c3_* profiles/$rnd/pmc_c3.json gpurun_out/profiles_$rnd/" \
   "trace1_c3|150|trace1 c3" "trace1_c4|200|trace1 c4" "trace1_c5|300|trace1 c5" \
   "bench_c3|240|python bench.py" \
   "bench_c3_driver|240|python bench.py --gpus 1 --steps 20 --warmup 5" \

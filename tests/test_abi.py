@@ -69,7 +69,7 @@ def test_product_has_no_oracle_dependency():
 
 
 def test_multi_gpu_and_diagnostic_entry_points_reject_bad_arguments_without_gpu():
-    """rt_render_tiled / rt_scene_copy / rt_wave_timeline / rt_chase_latency validate their
+    """rt_render_tiled / rt_scene_copy / rt_render_device_batch / rt_wave_timeline / rt_chase_latency validate their
     arguments before any device call (RT_ERR_INVALID_ARG = -1, message in rt_last_error)."""
     import numpy as np
     lib = rtamd.lib()
@@ -88,6 +88,9 @@ def test_multi_gpu_and_diagnostic_entry_points_reject_bad_arguments_without_gpu(
     assert lib.rt_render_tiled(two, 2, 0, 8, 1, 0, po) == -1     # zero width
     assert lib.rt_render_tiled(two, 2, 8, 8, 9, 0, po) == -1     # depth > RT_MAX_DEPTH
     assert lib.rt_scene_copy(None, None) == -1
+    cams = (rtamd.rt_params * 2)()
+    assert lib.rt_render_device_batch(None, 8, 8, 1, 0, None, cams, 2, po, 64, None) == -1   # no context
+    assert lib.rt_render_device_batch(None, 8, 8, 1, 0, None, None, 2, po, 64, None) == -1   # no params
     used = C.c_uint64()
     assert lib.rt_wave_timeline(None, 8, 8, 1, 0, 1, po, 256, C.byref(used)) == -1
     ms, waves = C.c_float(), C.c_uint64()

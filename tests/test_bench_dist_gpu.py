@@ -23,9 +23,12 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("i,extra", [(0, []), (1, ["--inflight", "1"]), (2, ["--band-rows", "16"]),
                                      (3, ["--gather", "native"]), (4, ["--gather", "native", "--inflight", "1"]),
-                                     (5, ["--gather", "torch"]), (6, ["--gather", "torch", "--gather-batch", "3"]),
-                                     (7, ["--gather", "native", "--gather-batch", "3"]),
-                                     (8, ["--gather", "torch", "--inflight", "1"])])
+                                     (5, ["--gather", "torch"]),
+                                     (6, ["--gather", "torch", "--gather-batch", "3", "--frames-per-launch", "1"]),
+                                     (7, ["--gather", "native", "--gather-batch", "3", "--frames-per-launch", "1"]),
+                                     (8, ["--gather", "torch", "--inflight", "1"]),
+                                     (9, ["--frames-per-launch", "1"]), (10, ["--frames-per-launch", "3"]),
+                                     (11, ["--gather", "torch", "--frames-per-launch", "3"])])
 def test_bench_dist_path_assembles_the_frame(i, extra):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29611 + i))
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist", "--config", "c2", "--direct", "--steps", "4",
@@ -71,12 +74,14 @@ def _ranks_on_one_gpu(n, extra, timeout=115):
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
+@pytest.mark.parametrize("n,fpl", [(2, 4), (3, 4), (2, 1), (3, 1)])
+def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n, fpl):
     """Every frame differs (orbiting camera); rank 0 observes each frame complete
     (rt_frame_present), checksums it right then, and every checksum and every frame it holds at
-    the end equal its own one-rank render of that frame's camera."""
-    p = _ranks_on_one_gpu(n, ["--steps", "24", "--orbit", "0.01", "--frame-check", "every"])
+    the end equal its own one-rank render of that frame's camera.  fpl: frames per launch (the
+    depth-1 default 4: each rank's bands of 4 frames in one launch, then each frame's put)."""
+    p = _ranks_on_one_gpu(n, ["--steps", "24", "--orbit", "0.01", "--frame-check", "every",
+                              "--frames-per-launch", str(fpl)])
     assert p.returncode == 0, _why(p)
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
@@ -85,7 +90,8 @@ def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n):
     fd, fc = res["config"]["frame_delivery"], res["config"]["frame_check"]
     assert fd["status"] == 0 and fd["frames_presented"] == fd["frames_rendered"] == 26
     assert fc["presented_frames_checksummed"] == 26 and fc["checksum_mismatches"] == 0, fc
-    assert fc["held_frames_checked"] == 8 and fc["distinct_cameras"] == 26, fc
+    # buffer sets: 2 x 4 frames in flight, each holding its last batch (fpl frames)
+    assert fc["held_frames_checked"] == (8 if fpl == 1 else 26) and fc["distinct_cameras"] == 26, fc
     assert res["config"]["gathered_frame_equals_single_rank_render"] is True, fc
     assert res["config"]["setup_skew_s"] is not None and res["config"]["band_exchange_fallback"] is None
     print(f"{n} ranks: set-up skew {res['config']['setup_skew_s']} s")
