@@ -399,7 +399,12 @@ def run(args, world, result_out=None):
     # and that allocation is uncached device memory (rt_shared_alloc): peers write it over
     # xGMI while rank 0's kernels poll and read it.  Other paths: a torch tensor.
     nfr_words = NB * B * h * w
-    sync_words = rtamd.frame_sync_words(NB, shard_n) if ipc else 0
+    # one completion set per frame buffer (buffer set j, frame s of its batch: q = j * B + s), so a
+    # frame's put waits only for the previous use of ITS buffer -- never for the present of another
+    # frame of the same batch (with B > 1 that would chain a batch's frames across ranks, and the
+    # puts waiting on it spin on the GPU)
+    NQ = NB * B
+    sync_words = rtamd.frame_sync_words(NQ, shard_n) if ipc else 0
     shm = None
 
     def torch_frames():
@@ -466,16 +471,16 @@ def run(args, world, result_out=None):
             drop_ipc()
         else:
             put_dst = [[fr_base + 4 * (j * B + s) * h * w for s in range(B)] for j in range(NB)]
-            sync_local = torch.zeros(NB, dtype=torch.int32, device=dev)   # this rank's per-set block counters
-            fsync = rtamd.FrameSync(w, h, tiling, shard_n, NB, fr_base + 4 * nfr_words, sync_local.data_ptr(),
+            sync_local = torch.zeros(NQ, dtype=torch.int32, device=dev)   # this rank's per-set block counters
+            fsync = rtamd.FrameSync(w, h, tiling, shard_n, NQ, fr_base + 4 * nfr_words, sync_local.data_ptr(),
                                     args.sync_timeout_ms)
             if args.shard:   # the N-1 shards no process puts: their arrivals never hold the present up
-                a0 = nfr_words + sync_words - NB * shard_n   # arrive[set][rank] ends the block
-                arrive = torch.full((NB, shard_n), -1, dtype=torch.int32, device=dev)   # 0xFFFFFFFF >= every use
+                a0 = nfr_words + sync_words - NQ * shard_n   # arrive[set][rank] ends the block
+                arrive = torch.full((NQ, shard_n), -1, dtype=torch.int32, device=dev)   # 0xFFFFFFFF >= every use
                 arrive[:, 0] = 0
                 rtamd.copy_device(fr_base + 4 * a0, arrive.data_ptr(), arrive.numel() * 4, streams[0].cuda_stream)
                 torch.cuda.synchronize(dev)
-            use = [0] * NB   # times set j has been filled
+            use = [0] * NQ   # times frame buffer q has been filled
     # frame checks: the camera index of every frame a set last held, and (--frame-check
     # every, rank 0) each presented frame's checksum, taken on its stream right after the
     # present saw it complete
@@ -595,22 +600,23 @@ def run(args, world, result_out=None):
         if ipc:      # this rank's bands into their rows of rank 0's frame, after the render;
             # rank 0 then waits (on this stream) until every rank's rows of the frame are in
             for s in range(nfr):
+                q = j * B + s
                 src = out_ptr[j][s]
                 if fault and frame_of[j][s] == fault_frame:
                     if args.inject_fault.startswith("drop-put"):
-                        use[j] += 1
+                        use[q] += 1
                         continue
                     src = out_ptr[(j + 1) % NB][s]   # another frame's bands
-                fsync.put(j, use[j], src, put_dst[j][s], sh[k])
+                fsync.put(q, use[q], src, put_dst[j][s], sh[k])
                 if rank == 0:   # the set goes back to the ranks after its consumer (the checksum)
-                    fsync.present(j, use[j], sh[k], release=not check_every)
+                    fsync.present(q, use[q], sh[k], release=not check_every)
                     if check_every:
                         n = frame_of[j][s]
                         if n < sums.numel():
                             rtamd.frame_checksum(put_dst[j][s], h * w, sums_ptr + 8 * n, sh[k])
                             checksummed.append(n)
-                        fsync.release(j, use[j], sh[k])
-                use[j] += 1
+                        fsync.release(q, use[q], sh[k])
+                use[q] += 1
             return
         if native:   # gather on the rt_comm's stream after the renders, rank 0's assembly after it
             xchg(j, nfr, outs_ptr[j], slots_ptr[j], fr_ptr[j], sh[k])

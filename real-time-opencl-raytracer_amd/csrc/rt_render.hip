@@ -769,12 +769,16 @@ __device__ __forceinline__ void set_status(uint32_t* sync, uint32_t code) {
                                          __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// rt_bands_put_sync: one block per local row.  Before writing set `set` for its use `use`
-// the block waits until rank 0 has presented the set's previous use (back-pressure: a peer
-// never overwrites a frame rank 0 has not yet observed complete).  After its row, every
-// block releases its stores at system scope (each XCD's L2 written back) and counts itself
-// on this rank's own counter for the set; the block that completes the count publishes
+// rt_bands_put_sync: at most kPutBlocks blocks, each copying every gridDim.x-th local row.
+// Before writing set `set` for its use `use` each block waits until rank 0 has presented the
+// set's previous use (back-pressure: a peer never overwrites a frame rank 0 has not yet observed
+// complete).  The grid is capped so that puts waiting on their sets hold few CU slots: a waiting
+// put with a block per row (1,080 at one rank) could fill a GPU shared by several ranks and starve
+// the very renders its wait depends on until the bound expires.  After its rows, every block
+// releases its stores at system scope (each XCD's L2 written back) and counts itself on this
+// rank's own counter for the set; the block that completes the count publishes
 // arrive[set][rank] = use + 1 with a system-scope release store.
+constexpr uint32_t kPutBlocks = 64;
 __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restrict__ frame,
                                                              const uint32_t* __restrict__ bands, uint32_t w,
                                                              uint32_t local_rows, uint32_t rank, uint32_t nranks,
@@ -782,7 +786,6 @@ __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restric
                                                              uint32_t nsets, uint32_t set, uint32_t use,
                                                              uint64_t timeout_ticks) {
     __shared__ uint32_t s_abort;
-    const uint32_t lr = blockIdx.x;
     if (threadIdx.x == 0) {
         uint32_t ab = 0;
         if (use > 0) {
@@ -801,22 +804,24 @@ __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restric
     }
     __syncthreads();
     if (s_abort) return;   // the set's arrival is never published: rank 0's present times out too
-    const uint64_t y = (uint64_t)(lr / band_rows * nranks + rank) * band_rows + lr % band_rows;
-    const uint32_t* src = bands + (uint64_t)lr * w;
-    uint32_t* dst = frame + y * w;
-    if ((w & 3u) == 0) {
-        const uint4* s4 = reinterpret_cast<const uint4*>(src);
-        uint4* d4 = reinterpret_cast<uint4*>(dst);
-        for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
-    } else {
-        for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t lr = blockIdx.x; lr < local_rows; lr += gridDim.x) {
+        const uint64_t y = (uint64_t)(lr / band_rows * nranks + rank) * band_rows + lr % band_rows;
+        const uint32_t* src = bands + (uint64_t)lr * w;
+        uint32_t* dst = frame + y * w;
+        if ((w & 3u) == 0) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(src);
+            uint4* d4 = reinterpret_cast<uint4*>(dst);
+            for (uint32_t i = threadIdx.x; i < w / 4; i += blockDim.x) d4[i] = s4[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) dst[i] = src[i];
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: this block's row is out of every cache
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: this block's rows are out of every cache
         const uint32_t prev = __hip_atomic_fetch_add(local + set, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1u == (use + 1u) * local_rows) {
+        if (prev + 1u == (use + 1u) * gridDim.x) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             __hip_atomic_store(sync + kSyncHead + nsets + set * nranks + rank, use + 1u, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1265,7 +1270,8 @@ int rt_bands_put_sync(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, ui
         return set_err(nullptr, "rt_bands_put_sync: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
     const uint32_t local_rows = (uint32_t)(npix / w);
     (void)hipGetLastError();   // an earlier call's error is not this launch's
-    hipLaunchKernelGGL(rtk::bands_put_sync_kernel, dim3(local_rows), dim3(256), 0, (hipStream_t)stream, d_frame, d_bands,
+    hipLaunchKernelGGL(rtk::bands_put_sync_kernel, dim3(std::min<uint32_t>(local_rows, rtk::kPutBlocks)), dim3(256), 0,
+                       (hipStream_t)stream, d_frame, d_bands,
                        w, local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows, d_sync, d_local,
                        (uint32_t)nsets, (uint32_t)set, use, timeout_ticks(timeout_ms));
     hipError_t e = hipGetLastError();
