@@ -23,7 +23,7 @@ for c in $cfgs; do
   for set in "${sets[@]}"; do
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $set -d $out/$c/p$i -o run --output-format csv -- \
-        python3 bench.py --config $c --steps 5 --warmup 1 --warmup-seconds 0 --no-cpu-baseline --no-roofline \
+        python3 bench.py --config $c --steps 8 --warmup 4 --warmup-seconds 0 --no-cpu-baseline --no-roofline \
         --inflight 1 "$@" > $out/$c/p$i.log 2>&1 || { echo "$c pass $i ($set) failed"; exit 1; }
   done
   for k in first_bounce_kernel first_bounce_batch_kernel wf_bounce_kernel wf_compact_sort_kernel; do

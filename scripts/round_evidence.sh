@@ -14,7 +14,7 @@ export GPU_MAX_HW_QUEUES=16
 trace1() {   # trace1 CONFIG: kernel trace + stats at one frame in flight
   cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-.}"
   rocprofv3 --kernel-trace --stats -d gpurun_out/$rnd/trace1_$1 -o run --output-format csv -- \
-    python3 bench.py --config $1 --steps 100 --warmup 5 --inflight 1 --no-cpu-baseline --no-roofline \
+    python3 bench.py --config $1 --steps 100 --warmup 5 --inflight 1 --frames-per-launch 1 --no-cpu-baseline --no-roofline \
     > gpurun_out/$rnd/trace1_$1.json 2> gpurun_out/$rnd/trace1_$1.err
 }
 export -f trace1
