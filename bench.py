@@ -66,8 +66,8 @@ def parse_args(argv=None):
                     help="diagnostic: batches of --gather-batch frames per stream at N = 1 too (no exchange)")
     ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="render each batch of K frames (K <= 8) with ONE launch (rt_render_device_batch: the "
-                         "longest tiles of all K frames first; depth-1 configs only); the frames in flight are then "
-                         "--inflight launches of K frames each.  0 (default): 4 for depth-1 configs, else 1")
+                         "longest tiles of all K frames first; depth 1, or the wavefront mode); the frames in flight are then "
+                         "--inflight launches of K frames each.  0 (default): 4 at depth 1, 8 in the wavefront mode, else 1")
     ap.add_argument("--hang-timeout", type=float, default=600.0,
                     help="N > 1: a rank that has not finished this many seconds after joining the process group "
                          "exits with status 3 (a stuck collective ends the run instead of hanging it)")
@@ -375,10 +375,14 @@ def run(args, world, result_out=None):
     # once per B frames
     # (ipc: a frame's put is one copy issued right after its render, no batching)
     B = max(1, args.gather_batch) if ((use_dist and not ipc) or args.local_batch) else 1
-    FPL = args.frames_per_launch if args.frames_per_launch > 0 else (4 if depth == 1 else 1)
+    # default frames per launch (profiles/r05/ab/frames_per_launch_ab.log): depth 1: 4 (C3 0.298 ms at 4,
+    # 0.300 at 8); the wavefront mode: 8 (C5 0.796 ms at 8, 0.802 at 4, 0.838 at 1)
+    FPL = args.frames_per_launch if args.frames_per_launch > 0 else (
+        4 if depth == 1 else 8 if (depth > 1 and (flags & 8) and cap == npx) else 1)
     if FPL > 1:   # a batch = the frames of one rt_render_device_batch launch (and of one gather at N > 1)
-        if depth != 1 or FPL > rtamd.RT_MAX_BATCH:
-            raise SystemExit(f"bench.py: --frames-per-launch needs a depth-1 config and K <= {rtamd.RT_MAX_BATCH}")
+        if depth < 1 or (depth > 1 and not (flags & 8)) or FPL > rtamd.RT_MAX_BATCH or (depth > 1 and cap != npx):
+            raise SystemExit(f"bench.py: --frames-per-launch needs depth 1 or the wavefront mode (with contiguous "
+                             f"frames at depth > 1) and K <= {rtamd.RT_MAX_BATCH}")
         B = FPL
     # buffer sets: batch i uses set i % NB.  At N > 1 the sets cycle 2F ways, so a batch never
     # renders into a set whose gather was issued less than F batches earlier: the gathers run

@@ -213,7 +213,8 @@ struct BatchCam {
 };
 struct BatchCams {
     BatchCam cam[kMaxBatch];
-    uint64_t stride;
+    uint64_t stride;      // pixels from one frame's output to the next
+    uint32_t frame_px;    // pixels of one frame (this rank's): frame f's first pixel in the launch's pixel space
 };
 
 __device__ __forceinline__ void leaf_range(const DevScene& S, uint32_t ref, int& off, int& cnt) {
@@ -1166,8 +1167,9 @@ template <int M> struct Kernels;
             return next ? (void*)NS::first_bounce_kernel<true, true, 1> : (void*)NS::first_bounce_kernel<true, false, 1>; \
         }                                                                                                  \
         static void* traced_bounce() { return (void*)NS::wf_bounce_kernel<true, 1>; }                     \
-        static void* batch(bool fast) {                                                                    \
-            return fast ? (void*)NS::first_bounce_batch_kernel<true> : (void*)NS::first_bounce_batch_kernel<false>; \
+        static void* batch(bool fast, bool next) {                                                         \
+            return fast ? (next ? (void*)NS::first_bounce_batch_kernel<true, true> : (void*)NS::first_bounce_batch_kernel<true, false>) \
+                        : (next ? (void*)NS::first_bounce_batch_kernel<false, true> : (void*)NS::first_bounce_batch_kernel<false, false>); \
         }                                                                                                  \
     };
 RTK_KERNELS(0, rtk_strict)
@@ -1178,8 +1180,8 @@ RTK_KERNELS(2, rtk_ref)
 static void* kernel_first(int m, bool fast, bool next) {
     return m == 0 ? Kernels<0>::first(fast, next) : m == 1 ? Kernels<1>::first(fast, next) : Kernels<2>::first(fast, next);
 }
-static void* kernel_batch(int m, bool fast) {
-    return m == 0 ? Kernels<0>::batch(fast) : m == 1 ? Kernels<1>::batch(fast) : Kernels<2>::batch(fast);
+static void* kernel_batch(int m, bool fast, bool next) {
+    return m == 0 ? Kernels<0>::batch(fast, next) : m == 1 ? Kernels<1>::batch(fast, next) : Kernels<2>::batch(fast, next);
 }
 static void* kernel_fused(int m, bool fast) {
     return m == 0 ? Kernels<0>::fused(fast) : m == 1 ? Kernels<1>::fused(fast) : Kernels<2>::fused(fast);
@@ -1653,10 +1655,17 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     if (batch) {
         if (nbatch < 1 || nbatch > rtk::kMaxBatch)
             return set_err(c, "rt_render_device_batch: nframes must be 1.." + std::to_string(rtk::kMaxBatch), RT_ERR_INVALID_ARG);
-        if (depth != 1) return set_err(c, "rt_render_device_batch: depth 1 only", RT_ERR_INVALID_ARG);
-        for (int32_t i = 1; i < nbatch; ++i)
+        if (depth < 1 || (depth > 1 && !(flags & RT_FLAG_WAVEFRONT)))
+            return set_err(c, "rt_render_device_batch: depth 1, or depth > 1 with RT_FLAG_WAVEFRONT", RT_ERR_INVALID_ARG);
+        for (int32_t i = 1; i < nbatch; ++i) {
             if (std::memcmp(&batch[i].scene_aabb_min, &batch[0].scene_aabb_min, 2 * sizeof(rt_float4)) != 0)
                 return set_err(c, "rt_render_device_batch: the frames' scene boxes differ", RT_ERR_INVALID_ARG);
+            // the bounce launches shade every frame's rays with one light (the reference's is a
+            // global, RayTracer.cpp:60)
+            if (depth > 1 && std::memcmp(&batch[i].light_pos, &batch[0].light_pos, sizeof(rt_float4)) != 0)
+                return set_err(c, "rt_render_device_batch: depth > 1 needs one light position for all frames",
+                               RT_ERR_INVALID_ARG);
+        }
         if (c->trace.on || c->tline.on)
             return set_err(c, "rt_render_device_batch: not with rt_fetch_counts / rt_wave_timeline", RT_ERR_INVALID_ARG);
     }
@@ -1671,6 +1680,11 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     if (npix < 0) return set_err(c, "rt_render_device: bad tiling", RT_ERR_INVALID_ARG);
     if (batch && bstride < (uint64_t)npix)
         return set_err(c, "rt_render_device_batch: frame_stride below the frame's pixels", RT_ERR_INVALID_ARG);
+    if (batch && depth > 1 && bstride != (uint64_t)npix)
+        return set_err(c, "rt_render_device_batch: depth > 1 needs contiguous frames (frame_stride = the frame's pixels)",
+                       RT_ERR_INVALID_ARG);
+    if (batch && (uint64_t)npix * K >= (1ull << 32))
+        return set_err(c, "rt_render_device_batch: more than 2^32 pixels in one launch", RT_ERR_INVALID_ARG);
     if (batch && d_aux) return set_err(c, "rt_render_device_batch: no aux planes", RT_ERR_INVALID_ARG);
     const bool aux = d_aux && d_aux->hits && d_aux->t && d_aux->rgb;
     if (d_aux && !aux && (d_aux->hits || d_aux->t || d_aux->rgb))
@@ -1728,7 +1742,7 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     O.t = aux ? d_aux->t : nullptr;
     O.rgb = aux ? d_aux->rgb : nullptr;
     O.overflow = c->d_overflow;
-    O.local_pixels = (uint64_t)npix;
+    O.local_pixels = (uint64_t)npix * K;   // a batch launch's pixel space: its frames one after the other
     O.fcount = nullptr;
     O.frame_rows = c->frame_rows && !batch ? 1u : 0u;
     O.wtime = nullptr;
@@ -1758,7 +1772,7 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     // frame counters, two parity sets: per bounce k (kBounceWords from kBounceWords k) its
     // queue size and its work cursor; [kRestartSlot] restarted traversals; then per queue
     // k = 1 .. its chunk sums and super-chunk sums (segmented queues, rtk::WQ)
-    const size_t nseg = (size_t)F.num_blocks * 4;   // bounce 0's waves; later queues have fewer groups
+    const size_t nseg = (size_t)F.num_blocks * 4 * K;   // bounce 0's waves (every frame's); later queues have fewer groups
     const size_t nchunk = (nseg + rtk::kChunkSegs - 1) / rtk::kChunkSegs;
     const size_t nsuper = (nseg + rtk::kSuperSegs - 1) / rtk::kSuperSegs;
     const size_t set_words = (kCounters + (depth > 1 ? (size_t)(depth - 1) * (nchunk + nsuper) : 0) + 31) & ~(size_t)31;
@@ -1899,9 +1913,11 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
                                              make_float4(Q.light_pos.x, Q.light_pos.y, Q.light_pos.z, 0.0f)};
                 }
                 C.stride = bstride;
-                void* bargs[] = {&S, &F, &O, &C};
-                if (ext_ev) HIPC(c, hipExtLaunchKernel(kernel_batch(math, fast), grid, block, bargs, 0, s, E.e[0], E.e[1], 0));
-                else HIPC(c, hipLaunchKernel(kernel_batch(math, fast), grid, block, bargs, 0, s));
+                C.frame_px = (uint32_t)npix;
+                void* bargs[] = {&S, &F, &O, &W, &C};
+                void* kb = kernel_batch(math, fast, depth > 1);
+                if (ext_ev) HIPC(c, hipExtLaunchKernel(kb, grid, block, bargs, 0, s, E.e[0], E.e[1], 0));
+                else HIPC(c, hipLaunchKernel(kb, grid, block, bargs, 0, s));
             } else if (ext_ev) {
                 HIPC(c, hipExtLaunchKernel(kernel_first(math, fast, depth > 1), grid, block, args, 0, s, E.e[0], E.e[1], 0));
             } else {

@@ -6,7 +6,9 @@ in the three math modes, with and without the shadow ray, for 1..RT_MAX_BATCH fr
 different cameras, on the first call of a geometry (the static order, a tile of every frame side
 by side) and on later calls (the longest-first order built over all frames' blocks), for a band
 of a multi-GPU tiling, and with a frame stride above the frame size (the gap untouched); C2 and
-C3 at full size.  Argument errors are refused before anything is enqueued."""
+C3 at full size; and depth 2-3 in the wavefront mode (one bounce-0 launch for all frames, then one
+launch per bounce over all frames' queues), C5 at full size.  Argument errors are refused before
+anything is enqueued."""
 import numpy as np
 import pytest
 
@@ -14,30 +16,30 @@ from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
-STRICT, HW, NO_SHADOW = 64, 2, 1
+STRICT, HW, NO_SHADOW, WAVEFRONT, WF_SORT = 64, 2, 1, 8, 32
 
 
 def _cams(mesh, w, h, k):
     return [mesh.camera_params(w, h, extra_alpha=0.07 * i, extra_beta=0.03 * i) for i in range(k)]
 
 
-def _singles(renderer, w, h, flags, cams, tiling=None, npx=None):
+def _singles(renderer, w, h, flags, cams, tiling=None, npx=None, depth=1):
     import torch
     npx = npx or w * h
     out = []
     for p in cams:
         renderer.set_params(p)
         dev = torch.full((npx,), -1, dtype=torch.int32, device="cuda")
-        renderer.render_device(w, h, 1, flags, dev.data_ptr(), tiling=tiling)
+        renderer.render_device(w, h, depth, flags, dev.data_ptr(), tiling=tiling)
         torch.cuda.synchronize()
         out.append(dev.cpu().numpy().view(np.uint32).copy())
     return out
 
 
-def _batch(renderer, w, h, flags, cams, stride, npx, tiling=None):
+def _batch(renderer, w, h, flags, cams, stride, npx, tiling=None, depth=1):
     import torch
     out = torch.full((len(cams) * stride,), -7, dtype=torch.int32, device="cuda")
-    renderer.render_device_batch(w, h, 1, flags, cams, out.data_ptr(), stride, tiling=tiling)
+    renderer.render_device_batch(w, h, depth, flags, cams, out.data_ptr(), stride, tiling=tiling)
     torch.cuda.synchronize()
     o = out.cpu().numpy().view(np.uint32)
     frames = [o[i * stride:i * stride + npx].copy() for i in range(len(cams))]
@@ -62,6 +64,34 @@ def test_batch_frames_equal_single_renders(renderer, k):
                     assert np.array_equal(got[i], want[i]), (k, w, h, flags, call, i, int(np.sum(got[i] != want[i])))
     t, _ = renderer.last_timing()
     assert t > 0.0
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 8])
+def test_wavefront_batch_frames_equal_single_renders(renderer, k):
+    """Depth 3 in the wavefront mode: bounce 0 of every frame in one launch, then each bounce
+    launch over all frames' queues (sorted and unsorted), every ray finishing in its own frame."""
+    import rtamd
+    d = load_golden("knot16k")
+    renderer.upload(rtamd.Scene.from_arrays(d))
+    mesh = rtamd.Mesh.torus_knot(128, 64)
+    for w, h in ((int(d["w"]), int(d["h"])), (123, 77), (640, 360)):
+        cams = _cams(mesh, w, h, k)
+        for flags in (WAVEFRONT, WAVEFRONT | WF_SORT, WAVEFRONT | STRICT, WAVEFRONT | WF_SORT | NO_SHADOW):
+            want = _singles(renderer, w, h, flags, cams, depth=3)
+            for call in range(2):
+                got, gaps_ok = _batch(renderer, w, h, flags, cams, w * h, w * h, depth=3)
+                assert gaps_ok
+                for i in range(k):
+                    assert np.array_equal(got[i], want[i]), (k, w, h, flags, call, i, int(np.sum(got[i] != want[i])))
+    # depth 2, and a band of a 2-way tiling
+    w, h = 333, 201
+    t = rtamd.rt_tiling(1, 2, 8, 0)
+    npx = rtamd.tiling_pixels(w, h, 1, 2, 8)
+    cams = _cams(mesh, w, h, 3)
+    want = _singles(renderer, w, h, WAVEFRONT | WF_SORT, cams, tiling=t, npx=npx, depth=2)
+    got, _ = _batch(renderer, w, h, WAVEFRONT | WF_SORT, cams, npx, npx, tiling=t, depth=2)
+    for i in range(3):
+        assert np.array_equal(got[i], want[i]), i
 
 
 def test_batch_band_tiling_and_mixed_calls(renderer):
@@ -97,7 +127,8 @@ def test_batch_argument_errors(renderer):
     cams = _cams(mesh, w, h, 9)
     for args, what in (((w, h, 1, 0, cams, out.data_ptr(), w * h), "nframes"),        # 9 > RT_MAX_BATCH
                        ((w, h, 1, 0, [], out.data_ptr(), w * h), "nframes"),          # 0 frames
-                       ((w, h, 3, 0, cams[:2], out.data_ptr(), w * h), "depth 1"),    # depth 3
+                       ((w, h, 3, 0, cams[:2], out.data_ptr(), w * h), "depth 1"),    # depth 3, not wavefront
+                       ((w, h, 3, WAVEFRONT, cams[:2], out.data_ptr(), w * h + 4), "contiguous"),
                        ((w, h, 1, 0, cams[:2], out.data_ptr(), w * h - 1), "stride"),
                        ((w, h, 1, STRICT | HW, cams[:2], out.data_ptr(), w * h), "exclude")):
         with pytest.raises(rtamd.RtError) as e:
@@ -108,9 +139,15 @@ def test_batch_argument_errors(renderer):
     with pytest.raises(rtamd.RtError) as e:
         renderer.render_device_batch(w, h, 1, 0, [cams[0], far], out.data_ptr(), w * h)
     assert "scene boxes" in str(e.value)
+    lit = mesh.camera_params(w, h)
+    lit.light_pos.y += 1.0
+    renderer.render_device_batch(w, h, 1, 0, [cams[0], lit], out.data_ptr(), w * h)   # depth 1: each frame's light
+    with pytest.raises(rtamd.RtError) as e:
+        renderer.render_device_batch(w, h, 3, WAVEFRONT, [cams[0], lit], out.data_ptr(), w * h)
+    assert "one light" in str(e.value)
 
 
-@pytest.mark.parametrize("name", ["c2", "c3"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c5"])
 def test_batch_full_size_frames_equal_single_renders(renderer, name):
     """BASELINE C2 / C3 scenes and frames, four cameras per launch (the config's camera and
     three translated copies: eye and image plane moved together), against one
@@ -119,7 +156,7 @@ def test_batch_full_size_frames_equal_single_renders(renderer, name):
     from test_fullsize_gpu import _config
     scene, params, cfg = _config(name)
     renderer.upload(scene)
-    w, h, flags = cfg["w"], cfg["h"], cfg["flags"]
+    w, h, flags, depth = cfg["w"], cfg["h"], cfg["flags"], cfg["depth"]
     cams = []
     for i in range(4):
         p = np.array(params, np.float32).copy()
@@ -127,10 +164,10 @@ def test_batch_full_size_frames_equal_single_renders(renderer, name):
         p[8:11] += dv     # c: the image plane's origin
         p[12:15] += dv    # campos
         cams.append(rtamd.array_to_params(p))
-    want = _singles(renderer, w, h, flags, cams)
+    want = _singles(renderer, w, h, flags, cams, depth=depth)
     assert not np.array_equal(want[0], want[1])
     for call in range(2):
-        got, gaps_ok = _batch(renderer, w, h, flags, cams, w * h, w * h)
+        got, gaps_ok = _batch(renderer, w, h, flags, cams, w * h, w * h, depth=depth)
         assert gaps_ok
         for i in range(4):
             assert np.array_equal(got[i], want[i]), (name, call, i, int(np.sum(got[i] != want[i])))
