@@ -377,10 +377,12 @@ def run(args, world, result_out=None):
     B = max(1, args.gather_batch) if ((use_dist and not ipc) or args.local_batch) else 1
     # default frames per launch (profiles/r05/ab/frames_per_launch_ab.log): depth 1: 4 (C3 0.298 ms at 4,
     # 0.300 at 8); the wavefront mode: 8 (C5 0.796 ms at 8, 0.802 at 4, 0.838 at 1)
-    FPL = args.frames_per_launch if args.frames_per_launch > 0 else (
-        4 if depth == 1 else 8 if (depth > 1 and (flags & 8) and cap == npx) else 1)
+    # (a wavefront batch needs contiguous frames: every rank's pixels a whole slot, decided alike on every rank)
+    wf_batch = depth > 1 and bool(flags & 8) and all(
+        rtamd.tiling_pixels(w, h, q, shard_n, args.band_rows) == cap for q in range(shard_n))
+    FPL = args.frames_per_launch if args.frames_per_launch > 0 else (4 if depth == 1 else 8 if wf_batch else 1)
     if FPL > 1:   # a batch = the frames of one rt_render_device_batch launch (and of one gather at N > 1)
-        if depth < 1 or (depth > 1 and not (flags & 8)) or FPL > rtamd.RT_MAX_BATCH or (depth > 1 and cap != npx):
+        if depth < 1 or (depth > 1 and not wf_batch) or FPL > rtamd.RT_MAX_BATCH:
             raise SystemExit(f"bench.py: --frames-per-launch needs depth 1 or the wavefront mode (with contiguous "
                              f"frames at depth > 1) and K <= {rtamd.RT_MAX_BATCH}")
         B = FPL
