@@ -988,7 +988,7 @@ def run(args, world, result_out=None):
     alg_bytes = frame_rays * bpr + 4.0 * frame_px            # reference-layout bytes per frame
     wavefront = depth > 1 and (flags & 8)
     ns = {0: "rtk_ref", 64: "rtk_strict", 2: "rtk_hw"}[math_flags]
-    kname = (f"{ns}::first_bounce_batch_kernel<true>" if FPL > 1
+    kname = (f"{ns}::first_bounce_batch_kernel<true, {'true' if depth > 1 else 'false'}>" if FPL > 1
              else f"{ns}::first_bounce_kernel<true, {'true' if depth > 1 else 'false'}, 0>" if (depth == 1 or wavefront)
              else f"{ns}::render_kernel<true>")
     # ---- roofline.  The path is a gather of 48-56 B records; its time is set by

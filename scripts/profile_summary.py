@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # C3 is depth 1: the single-bounce kernel (FASTONLY, no next ray, the product instantiation TR = 0),
 # or with bench.py's frames per launch > 1 (the depth-1 default) its batch form
 KERNEL_ONE = "first_bounce_kernel<true, false, 0>"
-KERNEL_BATCH = "first_bounce_batch_kernel<true>"
+KERNEL_BATCH = "first_bounce_batch_kernel<true, false>"
 KERNEL = KERNEL_ONE
 
 
