@@ -123,6 +123,7 @@ struct Frame {
     uint32_t* done;               // blocks finished so far (the last one builds lpt_next)
     uint32_t* zero_next;          // the other parity's frame counters, zeroed by this frame
     uint32_t nzero;
+    uint32_t* t0;                 // the launch's start (block 0's s_memrealtime), for RTK_LPT_BIAS
 };
 
 // A ray in flight between bounces: {pix, o.xyz}, {d.xyz, shadow_sum}, {colour.xyz, 3 * triangle it leaves from}.
@@ -429,6 +430,10 @@ __device__ __forceinline__ uint32_t lpt_key(uint32_t c) {
 #ifndef RTK_LPT_VEC
 #define RTK_LPT_VEC 1
 #endif
+#ifndef RTK_LPT_BIAS
+#define RTK_LPT_BIAS 0      // > 0: a block's cost for the next frame's order adds its start offset in the
+                            // launch >> RTK_LPT_BIAS (blocks that ran late measured shorter, same work)
+#endif
 #ifndef RTK_EPI_NOWAIT
 #define RTK_EPI_NOWAIT 0   // 1: the cost store and the counter add in flight together (profiles/r05/ab/epi_nowait_ab.log: equal)
 #endif
@@ -448,6 +453,12 @@ __device__ __forceinline__ void load_costs16(const uint32_t* cost, uint32_t q0, 
     // the wait "writes" the four results, so no use of them is scheduled above it
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : : "memory");
 }
+// RTK_LPT_BIAS: block 0 notes when the launch started (its first stamp; the frame's counter set
+// is zeroed before the frame, so 0 = not yet seen)
+__device__ __forceinline__ void note_launch_start(const Frame& F, uint32_t t_start) {
+    if (RTK_LPT_BIAS && F.tile_cost && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(F.t0, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uint32_t* scratch) {
     if (!F.tile_cost) return;   // launch-uniform
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -456,7 +467,12 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
     if (lane == 0) scratch[wave] = t_end - t_start + 1u;
     __syncthreads();
     if (tid == 0) {
-        const uint32_t c = max(max(scratch[0], scratch[1]), max(scratch[2], scratch[3]));
+        uint32_t c = max(max(scratch[0], scratch[1]), max(scratch[2], scratch[3]));
+        if (RTK_LPT_BIAS) {
+            const uint32_t T0 = __hip_atomic_load(F.t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t off = t_start - T0;
+            if (T0 != 0u && off < (1u << 26)) c += off >> RTK_LPT_BIAS;
+        }
         __hip_atomic_store(F.tile_cost + tb, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // RTK_EPI_NOWAIT: where the last block reads every cost exactly once (the keys kept in
         // LDS), the add does not wait for the store: the store and the add are in flight together
@@ -1018,7 +1034,8 @@ static hipError_t wait_stream(hipStream_t s) {
 // bounce kernel (rtk::grab_group)
 constexpr size_t kBounceWords = 32 + rtk::kCursorSet;
 constexpr size_t kRestartSlot = kBounceWords * (RT_MAX_DEPTH + 1);
-constexpr size_t kCounters = kRestartSlot + 1;
+constexpr size_t kT0Slot = kRestartSlot + 1;   // the launch's start (RTK_LPT_BIAS)
+constexpr size_t kCounters = kRestartSlot + 2;
 
 static int set_err(rt_ctx* c, const std::string& m, int code) {
     if (c) c->err = m; else g_err = m;
@@ -1787,6 +1804,7 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     F.nzero = (uint32_t)L.wcnt_set;   // all of it: the next frame may be deeper than this one
     auto sums = [&](int k) { return cnt + kCounters + (size_t)(k - 1) * (nchunk + nsuper); };   // queue k >= 1
     O.restarts = cnt + kRestartSlot;
+    F.t0 = cnt + kT0Slot;
 
     // static block order: a host-built table per block grid, made once (a new table goes into
     // a new allocation, so frames in flight that read another grid's table never wait)
