@@ -205,6 +205,12 @@ int rt_render_device(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_
 int rt_render_device_batch(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,
                            const rt_tiling* tiling, const rt_params* params, int32_t nframes, uint32_t* d_out,
                            uint64_t frame_stride, void* stream);
+/* The synchronous form (raytrace_gpgpu's launch + finish + blocking read-back, RayTracer.cpp:330-344,
+ * for nframes frames of one launch): out_bgr receives nframes * w*h packed pixels, frame i at
+ * out_bgr + i * w*h, the same as rt_render with params[i] for each.  Same depth / light rules as
+ * rt_render_device_batch.  Pinned, device-mapped out_bgr is written by the kernels directly. */
+int rt_render_batch(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_params* params,
+                    int32_t nframes, uint32_t* out_bgr);
 
 /* Number of pixels a rank owns under `tiling` (size of its output buffer). */
 int64_t rt_tiling_pixels(uint32_t w, uint32_t h, const rt_tiling* tiling);

@@ -1999,6 +1999,33 @@ int rt_render_device_batch(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uin
     return render_frames(c, w, h, depth, flags, tiling, d_out, nullptr, stream, params, nframes, frame_stride);
 }
 
+// rt_render_batch: rt_render's synchronous boundary for nframes frames of one launch (the frames
+// of a camera path the host already knows): into pinned, device-mapped memory directly, else
+// through the ctx's device frame buffer and one read-back of all frames.
+int rt_render_batch(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_params* params,
+                    int32_t nframes, uint32_t* out_bgr) {
+    if (!c || !out_bgr || !params || w == 0 || h == 0 || nframes < 1 || nframes > rtk::kMaxBatch)
+        return set_err(c, "rt_render_batch: invalid argument", RT_ERR_INVALID_ARG);
+    const size_t npix = (size_t)w * h;
+    HIPC(c, hipSetDevice(c->device));
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, out_bgr) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer) {
+        const int rc = render_frames(c, w, h, depth, flags, nullptr, (uint32_t*)pa.devicePointer, nullptr, c->stream,
+                                     params, nframes, npix);
+        if (rc) return rc;
+        HIPC(c, wait_stream(c->stream));
+        return RT_OK;
+    }
+    (void)hipGetLastError();   // pageable memory: not an error, the read-back path below
+    int rc = ensure(c, c->d_out, c->out_cap, npix * (size_t)nframes);
+    if (rc) return rc;
+    if ((rc = render_frames(c, w, h, depth, flags, nullptr, c->d_out, nullptr, c->stream, params, nframes, npix)))
+        return rc;
+    HIPC(c, hipMemcpyAsync(out_bgr, c->d_out, npix * (size_t)nframes * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, wait_stream(c->stream));
+    return RT_OK;
+}
+
 // rt_render: the reference's synchronous boundary (raytrace_gpgpu renders the whole frame, then
 // reads it back: RayTracer.cpp:330-344), with the readback overlapped with the rendering.
 //  * Pinned host memory the device can write (hipHostMalloc, or registered as mapped): the

@@ -7,13 +7,17 @@
 // Params, :671) then rt_render (launch + finish + blocking read-back, :330-344).
 // Optional PPM dumps replace the window.  With --gpus N (devices 0..N-1) or --devices a,b,...
 // (a list; a device may repeat) every frame goes to rt_render_tiled over one context per
-// entry instead: the scene is uploaded once and copied to the others (rt_scene_copy).
+// entry instead: the scene is uploaded once and copied to the others (rt_scene_copy).  With
+// --batch K the orbit's next K cameras go to ONE rt_render_batch call (the throughput mode: K frames
+// in one launch, read back together).
 //
 //   rt_frameloop [--dae F | --obj F | --scene cornell|knot|heightfield] [--bvh-cache F]
 //                [--width W] [--height H] [--depth D] [--frames N] [--drag DX DY]
 //                [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F] [--gpus N | --devices a,b,...]
+//                [--batch K]
 //
 // Prints "N.N fps" lines and a final JSON summary.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -29,7 +33,7 @@ namespace {
 struct Args {
     std::string dae, obj, scene = "heightfield", bvh_cache, ppm_dir;
     uint32_t w = 1024, h = 768;  // RayTracer.cpp:39-40 (WIDTH, HEIGHT)
-    int depth = 3, frames = 120, ppm_every = 0, device = 0;
+    int depth = 3, frames = 120, ppm_every = 0, device = 0, batch = 1;
     uint32_t flags = 0;
     float dx = 4.0f, dy = 0.0f;
     std::vector<int> devices;   // rt_render_tiled over these (empty: rt_render on --device)
@@ -40,7 +44,7 @@ int usage() {
                  "usage: rt_frameloop [--dae F | --obj F | --scene cornell|knot|heightfield] [--bvh-cache F]\n"
                  "                    [--width W] [--height H] [--depth D] [--frames N] [--drag DX DY]\n"
                  "                    [--ppm-dir DIR] [--ppm-every K] [--device I] [--flags F]\n"
-                 "                    [--gpus N | --devices a,b,...]\n");
+                 "                    [--gpus N | --devices a,b,...] [--batch K]\n");
     return 2;
 }
 
@@ -61,6 +65,7 @@ bool parse(int argc, char** argv, Args& a) {
         else if (k == "--ppm-every" && need(1)) a.ppm_every = std::atoi(argv[++i]);
         else if (k == "--device" && need(1)) a.device = std::atoi(argv[++i]);
         else if (k == "--flags" && need(1)) a.flags = (uint32_t)std::strtoul(argv[++i], nullptr, 0);
+        else if (k == "--batch" && need(1)) a.batch = std::atoi(argv[++i]);
         else if (k == "--gpus" && need(1)) {
             const int n = std::atoi(argv[++i]);
             if (n < 1 || n > 64) return false;
@@ -79,7 +84,8 @@ bool parse(int argc, char** argv, Args& a) {
             if (a.devices.empty() || a.devices.size() > 64) return false;
         } else return false;
     }
-    return a.w > 0 && a.h > 0 && a.frames > 0 && a.depth >= 0 && a.depth <= RT_MAX_DEPTH;
+    return a.w > 0 && a.h > 0 && a.frames > 0 && a.depth >= 0 && a.depth <= RT_MAX_DEPTH && a.batch >= 1 &&
+           a.batch <= RT_MAX_BATCH && (a.batch == 1 || a.devices.size() <= 1);
 }
 
 // Packed pixels are b<<16 | g<<8 | r (volumeRender.cl:186-195); row 0 is the first image row.
@@ -151,30 +157,44 @@ int main(int argc, char** argv) {
             return 1;
         }
     const int32_t nctx = (int32_t)ctxs.size();
+    // batches deeper than one bounce run in the wavefront mode (the same pixels as the fused kernel)
+    if (a.batch > 1 && a.depth > 1) a.flags |= RT_FLAG_WAVEFRONT;
 
     rt_camera* cam = rt_camera_create(200.0f);
-    std::vector<uint32_t> px((size_t)a.w * a.h);
+    const size_t npx = (size_t)a.w * a.h;
+    std::vector<uint32_t> px(npx * (size_t)a.batch), one;
+    std::vector<rt_params> cams((size_t)a.batch);
     int frames_in_second = 0, total = 0;
     double kernel_ms_sum = 0.0;
     auto t0 = clk::now(), tsec = t0;
-    for (int f = 0; f < a.frames; ++f) {
-        if (f > 0) rt_camera_add_rotate(cam, a.dx * 0.25f / 100.0f, a.dy * 0.25f / 100.0f);  // motion()
-        rt_params p;
-        rt_camera_frame_params(cam, mesh, a.w, a.h, nullptr, nullptr, &p);   // updateCamera()
-        if ((rc = rt_set_params(ctx, &p)) != RT_OK ||
-            (rc = nctx > 1 ? rt_render_tiled(ctxs.data(), nctx, a.w, a.h, a.depth, a.flags, px.data())
-                           : rt_render(ctx, a.w, a.h, a.depth, a.flags, px.data(), nullptr)) != RT_OK) {
-            std::fprintf(stderr, "frame %d: %s\n", f, rt_last_error(ctx));
+    for (int f0 = 0; f0 < a.frames; f0 += a.batch) {
+        const int k = std::min(a.batch, a.frames - f0);   // this call's frames f0 .. f0 + k - 1
+        for (int i = 0; i < k; ++i) {
+            if (f0 + i > 0) rt_camera_add_rotate(cam, a.dx * 0.25f / 100.0f, a.dy * 0.25f / 100.0f);  // motion()
+            rt_camera_frame_params(cam, mesh, a.w, a.h, nullptr, nullptr, &cams[(size_t)i]);     // updateCamera()
+        }
+        if (a.batch > 1) {
+            rc = rt_render_batch(ctx, a.w, a.h, a.depth, a.flags, cams.data(), k, px.data());
+        } else if ((rc = rt_set_params(ctx, &cams[0])) == RT_OK) {
+            rc = nctx > 1 ? rt_render_tiled(ctxs.data(), nctx, a.w, a.h, a.depth, a.flags, px.data())
+                          : rt_render(ctx, a.w, a.h, a.depth, a.flags, px.data(), nullptr);
+        }
+        if (rc != RT_OK) {
+            std::fprintf(stderr, "frame %d: %s\n", f0, rt_last_error(ctx));
             return 1;
         }
         float kt = 0.0f, kk = 0.0f;
-        if (rt_last_timing(ctx, &kt, &kk) == RT_OK) kernel_ms_sum += kt;
-        ++frames_in_second;
-        ++total;
-        if (a.ppm_every > 0 && !a.ppm_dir.empty() && f % a.ppm_every == 0) {
-            char name[64];
-            std::snprintf(name, sizeof name, "/frame_%05d.ppm", f);
-            if (!write_ppm(a.ppm_dir + name, px, a.w, a.h)) std::fprintf(stderr, "cannot write %s\n", name);
+        if (rt_last_timing(ctx, &kt, &kk) == RT_OK) kernel_ms_sum += kt;   // the call's kernels (k frames)
+        frames_in_second += k;
+        total += k;
+        for (int i = 0; i < k; ++i) {
+            const int f = f0 + i;
+            if (a.ppm_every > 0 && !a.ppm_dir.empty() && f % a.ppm_every == 0) {
+                char name[64];
+                std::snprintf(name, sizeof name, "/frame_%05d.ppm", f);
+                one.assign(px.begin() + (ptrdiff_t)(npx * (size_t)i), px.begin() + (ptrdiff_t)(npx * (size_t)(i + 1)));
+                if (!write_ppm(a.ppm_dir + name, one, a.w, a.h)) std::fprintf(stderr, "cannot write %s\n", name);
+            }
         }
         const auto now = clk::now();
         const double since = std::chrono::duration<double>(now - tsec).count();
@@ -188,9 +208,9 @@ int main(int argc, char** argv) {
     const double wall = std::chrono::duration<double>(clk::now() - t0).count();
     std::printf("{\"frames\": %d, \"width\": %u, \"height\": %u, \"depth\": %d, \"fps\": %.2f, \"ms_per_frame\": %.4f, "
                 "\"kernel_ms_per_frame\": %.4f, \"triangles\": %d, \"bvh_nodes\": %d, \"bvh_cached\": %s, "
-                "\"bvh_seconds\": %.3f, \"contexts\": %d}\n",
+                "\"bvh_seconds\": %.3f, \"contexts\": %d, \"frames_per_call\": %d}\n",
                 total, a.w, a.h, a.depth, total / wall, 1e3 * wall / total, kernel_ms_sum / total,
-                mv.num_indices / 3, bv.num_nodes, cached ? "true" : "false", bvh_s, nctx);
+                mv.num_indices / 3, bv.num_nodes, cached ? "true" : "false", bvh_s, nctx, a.batch);
     rt_camera_destroy(cam);
     for (rt_ctx* c : ctxs) rt_destroy(c);
     rt_bvh_destroy(bvh);

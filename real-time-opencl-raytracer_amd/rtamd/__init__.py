@@ -82,7 +82,7 @@ class rt_bvh_view(C.Structure):
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
 ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_tiled", "rt_scene_copy",
-               "rt_render_device", "rt_render_device_batch",
+               "rt_render_device", "rt_render_device_batch", "rt_render_batch",
                "rt_tiling_pixels", "rt_assemble_bands", "rt_assemble_bands_batch", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
                "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
                "rt_frame_ready_wait", "rt_ipc_export", "rt_ipc_open", "rt_ipc_close", "rt_bands_put",
@@ -126,6 +126,7 @@ def lib() -> C.CDLL:
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
             "rt_render_device_batch": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), C.POINTER(rt_params), i32,
                                                  vp, C.c_uint64, vp]),
+            "rt_render_batch": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_params), i32, vp]),
             "rt_tiling_pixels": (C.c_int64, [u32, u32, C.POINTER(rt_tiling)]),
             "rt_assemble_bands": (C.c_int, [vp, vp, C.c_uint64, u32, u32, i32, i32, vp]),
             "rt_assemble_bands_batch": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, i32, u32, u32, i32, i32, vp]),
@@ -584,6 +585,19 @@ class Renderer:
         _check(lib().rt_render_device_batch(self._h, w, h, depth, flags, None if tiling is None else C.byref(tiling),
                                             arr, len(params), C.c_void_p(d_out_ptr), frame_stride,
                                             C.c_void_p(stream or None)), self._h)
+
+    def render_batch(self, w: int, h: int, depth: int, flags: int, params, out_ptr: Optional[int] = None):
+        """rt_render_batch: len(params) frames in one launch, synchronous; returns a (k, h*w) uint32
+        array, or fills the host memory at out_ptr (k * w*h uint32, pageable or pinned)."""
+        arr = (rt_params * max(1, len(params)))()
+        for i, p in enumerate(params):
+            arr[i] = p if isinstance(p, rt_params) else array_to_params(p)
+        out = None
+        if out_ptr is None:
+            out = np.zeros((max(1, len(params)), w * h), np.uint32)
+            out_ptr = out.ctypes.data
+        _check(lib().rt_render_batch(self._h, w, h, depth, flags, arr, len(params), C.c_void_p(out_ptr)), self._h)
+        return out
 
     def batch_launcher(self, w, h, depth, flags, tiling: Optional[rt_tiling] = None):
         """A callable (params_array, n, d_out_ptr, frame_stride, stream) -> None that enqueues n frames

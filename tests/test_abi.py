@@ -91,6 +91,7 @@ def test_multi_gpu_and_diagnostic_entry_points_reject_bad_arguments_without_gpu(
     cams = (rtamd.rt_params * 2)()
     assert lib.rt_render_device_batch(None, 8, 8, 1, 0, None, cams, 2, po, 64, None) == -1   # no context
     assert lib.rt_render_device_batch(None, 8, 8, 1, 0, None, None, 2, po, 64, None) == -1   # no params
+    assert lib.rt_render_batch(None, 8, 8, 1, 0, cams, 2, po) == -1                          # no context
     used = C.c_uint64()
     assert lib.rt_wave_timeline(None, 8, 8, 1, 0, 1, po, 256, C.byref(used)) == -1
     ms, waves = C.c_float(), C.c_uint64()

@@ -127,3 +127,36 @@ def test_multi_context_frames_match_the_render_abi(tmp_path, depth):
         ren.set_params(p)
         assert np.array_equal(_read_ppm(tmp_path / f"frame_{f:05d}.ppm"), _rgb(ren.render(w, h, depth=depth), w, h)), f
     ren.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth,batch", [(1, 4), (3, 3)])
+def test_batched_frames_match_the_render_abi(tmp_path, depth, batch):
+    """--batch K: the orbit's next K cameras in one rt_render_batch call (K frames in one launch;
+    depth 3 in the wavefront mode); every frame equals rt_render's for its camera, including the
+    last, part-filled call (7 frames)."""
+    import rtamd
+    w, h, frames, dx, dy = 160, 120, 7, 7.0, -3.0
+    summary = _run_tool(tmp_path, w, h, depth, frames, dx, dy, 0, extra=("--batch", str(batch)))
+    assert summary["frames_per_call"] == batch
+    m = rtamd.Mesh.cornell()
+    ren = rtamd.Renderer(0)
+    ren.upload(rtamd.Scene.from_mesh(m, m.build_sbvh()))
+    cams = _orbit_params(m, w, h, frames, dx, dy)
+    for f, p in enumerate(cams):
+        if f % 2:
+            continue
+        ren.set_params(p)
+        assert np.array_equal(_read_ppm(tmp_path / f"frame_{f:05d}.ppm"), _rgb(ren.render(w, h, depth=depth), w, h)), f
+    # rt_render_batch through ctypes, into pageable and pinned memory
+    import torch
+    flags = rtamd.RT_FLAG_WAVEFRONT if depth > 1 else 0
+    got = ren.render_batch(w, h, depth, flags, cams[:batch])
+    pin = torch.zeros(batch * w * h, dtype=torch.int32, pin_memory=True)
+    ren.render_batch(w, h, depth, flags, cams[:batch], out_ptr=pin.data_ptr())
+    for i in range(batch):
+        ren.set_params(cams[i])
+        want = ren.render(w, h, depth=depth)
+        assert np.array_equal(got[i], want), i
+        assert np.array_equal(pin.numpy().view(np.uint32)[i * w * h:(i + 1) * w * h], want), i
+    ren.close()
