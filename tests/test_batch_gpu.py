@@ -16,7 +16,7 @@ from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
-STRICT, HW, NO_SHADOW, WAVEFRONT, WF_SORT = 64, 2, 1, 8, 32
+STRICT, HW, NO_SHADOW, WAVEFRONT, WF_SORT, STATIC_ORDER, EXACT_DIV = 64, 2, 1, 8, 32, 16, 4
 
 
 def _cams(mesh, w, h, k):
@@ -55,7 +55,7 @@ def test_batch_frames_equal_single_renders(renderer, k):
     mesh = rtamd.Mesh.torus_knot(128, 64)
     for w, h in ((int(d["w"]), int(d["h"])), (123, 77), (640, 360)):
         cams = _cams(mesh, w, h, k)
-        for flags in (0, NO_SHADOW, STRICT, STRICT | NO_SHADOW, HW):
+        for flags in (0, NO_SHADOW, STRICT, STRICT | NO_SHADOW, HW, STATIC_ORDER, EXACT_DIV):
             want = _singles(renderer, w, h, flags, cams)
             for call in range(3):   # call 0: static order; then the adaptive order of all frames
                 got, gaps_ok = _batch(renderer, w, h, flags, cams, w * h + 37, w * h)
@@ -76,7 +76,8 @@ def test_wavefront_batch_frames_equal_single_renders(renderer, k):
     mesh = rtamd.Mesh.torus_knot(128, 64)
     for w, h in ((int(d["w"]), int(d["h"])), (123, 77), (640, 360)):
         cams = _cams(mesh, w, h, k)
-        for flags in (WAVEFRONT, WAVEFRONT | WF_SORT, WAVEFRONT | STRICT, WAVEFRONT | WF_SORT | NO_SHADOW):
+        for flags in (WAVEFRONT, WAVEFRONT | WF_SORT, WAVEFRONT | STRICT, WAVEFRONT | WF_SORT | NO_SHADOW, WAVEFRONT | HW,
+                      WAVEFRONT | WF_SORT | STATIC_ORDER):
             want = _singles(renderer, w, h, flags, cams, depth=3)
             for call in range(2):
                 got, gaps_ok = _batch(renderer, w, h, flags, cams, w * h, w * h, depth=3)
