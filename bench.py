@@ -48,6 +48,11 @@ def parse_args(argv=None):
     ap.add_argument("--orbit", type=float, default=0.0,
                     help="moving camera: add_rotate(ORBIT, 0) radians per frame, as the reference's mouse "
                          "drag does (RayTracer.cpp:553-565); 0 = the static default camera")
+    ap.add_argument("--jitter", type=int, default=16,
+                    help="static camera: cycle through this many sub-pixel jittered copies of it (frame n: camera "
+                         "n %% J, the image plane shifted by a Halton(2,3) offset inside one pixel; camera 0 is the "
+                         "unjittered one), so no two frames of a launch or of the frames in flight trace the same "
+                         "rays; 1 = every frame the identical default camera")
     ap.add_argument("--band-rows", type=int, default=8,
                     help="rows per screen band (bands dealt round-robin to ranks; 8 = one tile row)")
     ap.add_argument("--dist", action="store_true", help="use the process-group gather path even at N = 1")
@@ -179,6 +184,29 @@ def host_cpu_share():
             "omp_num_threads": omp, "os_cpu_count": os.cpu_count()}
 
 
+def halton(i, b):
+    f, x = 1.0, 0.0
+    while i > 0:
+        f /= b
+        x += f * (i % b)
+        i //= b
+    return x
+
+
+def jittered_cameras(p, w, h, n):
+    """n copies of the camera Params p (32 floats), copy k with its image plane shifted by a
+    sub-pixel offset (Halton(2,3) point k, centred: k = 0 is p itself): image_pos = c + a xf + b yf
+    with xf = (x - 0.5) / w (volumeRender.cl:1169-1190), so c + a dx / w + b dy / h moves every
+    primary ray by (dx, dy) pixels, |dx|, |dy| < 0.5."""
+    import numpy as np
+    out = np.repeat(p.reshape(1, 32), n, axis=0).astype(np.float32)
+    q = p.reshape(8, 4).astype(np.float64)
+    for k in range(1, n):
+        dx, dy = halton(k, 2) - 0.5, halton(k, 3) - 0.5
+        out[k, 8:11] = (q[2, :3] + q[0, :3] * (dx / w) + q[1, :3] * (dy / h)).astype(np.float32)
+    return out
+
+
 def _hang_exit(rank, seconds):
     print(f"bench.py: rank {rank} still running {seconds:.0f} s after joining the process group; exiting",
           file=sys.stderr, flush=True)
@@ -293,7 +321,7 @@ def run(args, world, result_out=None):
                 plist.append(rtamd.params_to_array(cam.params(mesh, w, h)))
             ptab = np.stack(plist)
         else:
-            ptab = rtamd.params_to_array(mesh.camera_params(w, h))[None, :]
+            ptab = jittered_cameras(rtamd.params_to_array(mesh.camera_params(w, h)), w, h, max(1, args.jitter))
     scene_bytes = 0
     if world > 1:
         nb = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -514,6 +542,12 @@ def run(args, world, result_out=None):
         return int((hv != -2).sum().item()), int((hv[:, 0, 0] != -2).sum().item())
 
     rays_f0, prim_f0 = count_rays(ptab[0])
+    ray_cache = {0: (rays_f0, prim_f0)}
+
+    def rays_of(cam):   # (rays, primary rays) of camera index cam, counted once
+        if cam not in ray_cache:
+            ray_cache[cam] = count_rays(ptab[cam])
+        return ray_cache[cam]
 
     # rank 0's frame checks: its own one-rank render of a camera, and every frame a buffer set
     # holds against it (under --orbit every frame differs, so a band in the wrong frame shows)
@@ -572,7 +606,8 @@ def run(args, world, result_out=None):
     sh = [st.cuda_stream for st in streams]
     out_ptr = [[o[s].data_ptr() for s in range(B)] for o in outs]
     outs_ptr = [o.data_ptr() for o in outs]
-    orbit_params = [rtamd.array_to_params(p) for p in ptab] if args.orbit else None
+    # per-frame cameras (orbit, or the jittered copies of the static camera): frame n has camera n % L
+    orbit_params = [rtamd.array_to_params(p) for p in ptab] if ptab.shape[0] > 1 else None
     set_params = rtamd.lib().rt_set_params
     hdl = r._h
     if native:
@@ -799,14 +834,40 @@ def run(args, world, result_out=None):
         r.set_params(ptab[0])
         batch_check = {"frames_checked": n_checked, "equal_to_single_renders": batch_ok}
 
+    # (untimed for `value`) the same frames one per launch (rt_render_device: what a caller that has
+    # only one frame at a time to give can get with F frames in flight), same cameras, same streams
+    one_per_launch = None
+    if FPL > 1 and not use_dist and not args.shard:
+        nf = max(args.steps, 64)
+        for cam in {i % L for i in range(32, nf + 32)}:
+            rays_of(cam)   # counted before the timed frames
+        torch.cuda.synchronize(dev)
+        t1 = 0.0
+        rays1 = 0
+        for i in range(nf + 32):
+            if i == 32:
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+            if orbit_params is not None:
+                set_params(hdl, orbit_params[i % len(orbit_params)])
+            launch(out_ptr[i % NB][0], sh[i % F])
+            if i >= 32:
+                rays1 += rays_of(i % L)[0] if L > 1 else rays_f0
+        torch.cuda.synchronize(dev)
+        el1 = time.perf_counter() - t1
+        r.set_params(ptab[0])
+        one_per_launch = {"ms_per_frame": round(el1 / nf * 1e3, 4), "mrays_per_s": round(rays1 / el1 / 1e6, 1),
+                          "frames": nf, "frames_in_flight": F,
+                          "how": "rt_render_device, one frame per launch, same cameras and streams (untimed for value)"}
+
     total_frames = warmup_frames + args.steps
     # frame n was rendered with camera n % L (the orbit table wraps when the time-based
     # warm-up ran past it; a static camera has L = 1)
     # rays of the timed frames (untimed: one aux render per distinct camera)
-    if args.orbit:
+    if L > 1:
         rays_local = prim_local = 0
         for n in range(warmup_frames, total_frames):
-            a, b = count_rays(ptab[n % L])
+            a, b = rays_of(n % L)
             rays_local += a
             prim_local += b
         r.set_params(ptab[0])
@@ -847,9 +908,9 @@ def run(args, world, result_out=None):
                    int(got[n]) != reference(n % L)]
             frame_check.update({"presented_frames_checksummed": len(checksummed), "checksum_mismatches": len(bad),
                                 "mismatched_frames": bad[:16]})
+            frame_ok = frame_ok and not bad
         if held_bad:
             frame_check["held_frames_differing"] = held_bad[:16]
-            frame_ok = frame_ok and not bad
         r.set_params(ptab[0])
 
 
@@ -1066,8 +1127,10 @@ def run(args, world, result_out=None):
         roof = {"bound": "hbm", "unit": "GB/s", "achieved": hbm["achieved_gbs"], "peak": HBM_PEAK_GBS,
                 "frac": round(hbm["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
                 "roof": "HBM (no fetch counts for this run)"}
-    roof.update({"hbm": hbm, "stream_copy_gbs": round(stream_copy_gbs, 1), "kernel_ms": round(kernel_ms_avg, 4),
-                 "frame_kernels_ms": round(frame_ms_avg, 4), "launches_overlap": F > 1, "kernel": kname,
+    # HIP-event times of one timing entry = one launch group (FPL frames): per launch and per frame
+    roof.update({"hbm": hbm, "stream_copy_gbs": round(stream_copy_gbs, 1),
+                 "kernel_ms_per_launch": round(kernel_ms_avg, 4), "kernel_ms_per_frame": round(kernel_ms_avg / FPL, 4),
+                 "launch_kernels_ms": round(frame_ms_avg, 4), "launches_overlap": F > 1, "kernel": kname,
                  "frames_per_launch": FPL,
                  "records_per_ray_oracle": round(rec_inner + rec_tri, 2)})
     # HBM traffic: PMC counters need rocprofv3, so they come from separate profiling runs of this
@@ -1110,7 +1173,11 @@ def run(args, world, result_out=None):
                    "bvh_nodes": int(bvh.nodes.shape[0]), "width": w, "height": h, "depth": depth,
                    "shadow": not (flags & 1), "math": MATH[math_flags], "flags": flags,
                    "camera": (f"orbit: add_rotate({args.orbit}, 0) per frame (RayTracer.cpp:553-565)" if args.orbit
-                              else "static default camera (Camera.cpp:6-19)"),
+                              else f"static default camera (Camera.cpp:6-19), frame n jittered by Halton(2,3) "
+                                   f"sub-pixel offset n % {L} (camera 0 unjittered)" if L > 1
+                              else "static default camera (Camera.cpp:6-19), every frame identical"),
+                   "batch_cameras": ("distinct" if (L >= FPL * F or FPL == 1 and L >= F) else
+                                     "identical" if L == 1 else "partly repeated"),
                    "block_order": "static" if flags & 16 else "adaptive longest-first from the previous frame",
                    "rays_per_frame": round(frame_rays, 1),
                    "primary_rays_per_frame": round(prim_total / args.steps, 1),
@@ -1158,6 +1225,8 @@ def run(args, world, result_out=None):
         res["config"]["host_boundary"] = host_boundary
     if frame_latency is not None:
         res["config"]["frame_latency"] = frame_latency
+    if one_per_launch is not None:
+        res["config"]["one_frame_per_launch"] = one_per_launch
     print(json.dumps(res), file=result_out or sys.stdout, flush=True)
     if batch_check is not None and not batch_check["equal_to_single_renders"]:
         raise SystemExit("bench.py: a batch-launch frame differs from its single render")

@@ -169,13 +169,26 @@ int rt_render(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags
  * (rt_upload_scene, or rt_scene_copy from one that does).  The camera is ctxs[0]'s
  * (rt_set_params; copied to the others).  The frame is cut into 8-row bands dealt round-robin
  * (band b -> ctxs[b % n]); every context renders its bands on its own stream and
- * writes each pixel straight into its row of the host frame: the caller's out_bgr when it is
- * pinned memory the devices can write (hipHostMalloc, or registered mapped), else a pinned
- * staging frame of ctxs[0] copied to out_bgr after the join.  Synchronous: returns when every
- * context is done and out_bgr holds the w*h packed pixels -- the same pixels as rt_render with
- * the same flags.  n == 1 is rt_render.  Errors are reported on ctxs[0] (rt_last_error). */
+ * writes each pixel straight into its row of the host frame: the caller's out_bgr when every
+ * context's device maps it (hipHostGetDevicePointer on each device: hipHostMalloc'd portable
+ * memory, or memory registered and mapped for all of them), else a portable pinned staging frame
+ * of ctxs[0] copied to out_bgr after the join.  ctxs[1..n-1] enqueue and wait on host threads of
+ * their own (started on first use, spinning between frames, stopped by rt_destroy), ctxs[0] on
+ * the caller's thread (RTAMD_TILED_WORKERS=0: all on the caller's thread, in turn).  Synchronous:
+ * returns when every context is done and out_bgr holds the w*h packed pixels -- the same pixels
+ * as rt_render with the same flags.  n == 1 is rt_render.  Errors are reported on ctxs[0]
+ * (rt_last_error). */
 int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,
                     uint32_t* out_bgr);
+/* rt_render_tiled's choice of frame, on its own so that it is testable without a GPU: given for
+ * each of n contexts the device address its device resolved for the caller's host buffer (0 = that
+ * device cannot address it), 1 when every context can write the buffer directly (all resolved,
+ * 16-B aligned), 0 when the frame must go through the pinned staging frame. */
+int32_t rt_tiled_direct_ok(int32_t n, const uint64_t* dev_addrs);
+/* Host steady-clock nanoseconds at the start and end of the context's last rt_render_device
+ * enqueue (rt_render_tiled's parts included): the spread of the starts over a tiled frame's
+ * contexts is how far apart their GPUs start. */
+int rt_last_enqueue_time(rt_ctx* ctx, uint64_t* begin_ns, uint64_t* end_ns);
 /* Copies src's uploaded scene (its device layouts) into dst: device to device on one GPU,
  * peer to peer over xGMI between two (hipMemcpyPeer), with no host round trip and no second
  * BVH build (initRayTrace's upload, RayTracer.cpp:942-984, done once per node).  Synchronous. */

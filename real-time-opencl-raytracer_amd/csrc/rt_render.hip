@@ -34,12 +34,16 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_abi.h"
@@ -78,6 +82,12 @@
 #endif
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
+#endif
+#ifndef RTK_LEAFRUN
+#define RTK_LEAFRUN 0       // A/B: a wave past RTK_LEAFRUN_TRIPS main-loop trips tests a leaf's remaining
+#endif                      // triangles in one trip (the long waves that set a frame's latency)
+#ifndef RTK_LEAFRUN_TRIPS
+#define RTK_LEAFRUN_TRIPS 64
 #endif
 
 namespace rtk {
@@ -306,11 +316,23 @@ __device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
 // [0] / [1] closest-hit main-loop / wave-uniform-prologue trips, [2] / [3] the same for the shadow
 // (any-hit) traversal, [4] s_memrealtime when the closest-hit traversal returned, [5] when the
 // shading was done (the shadow traversal starts), [6] when the closest-hit traversal started,
-// [7] when its wave-uniform prologue ended; trips counted and times taken by the wave's
-// first active lane.  (In a persistent bounce wave: trips over all its groups, times of its last.)
-constexpr uint32_t kTlWords = 8, kTlRecord = 16;
+// [7] when its wave-uniform prologue ended; with RTK_TL_SPLIT (a diagnostic build) [8] / [9] the
+// closest-hit / shadow main loop's ticks between issuing a trip's record loads and their arrival
+// (the trip's memory wait), [10] / [11] those trips' count whose wait was >= kTlLongWait ticks;
+// trips counted and times taken by the wave's first active lane.  (In a persistent bounce wave:
+// trips over all its groups, times of its last.)
+#ifndef RTK_TL_SPLIT
+#define RTK_TL_SPLIT 0
+#endif
+constexpr uint32_t kTlWords = 12, kTlRecord = 20, kTlLongWait = 25;
 __device__ __forceinline__ void timeline_step(uint32_t* c, int which) {
     if ((uint32_t)(threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) c[which] += 1u;
+}
+__device__ __forceinline__ void timeline_wait(uint32_t* c, int which, uint32_t ticks) {
+    if ((uint32_t)(threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) {
+        c[8 + which] += ticks;
+        c[10 + which] += ticks >= kTlLongWait ? 1u : 0u;
+    }
 }
 __device__ __forceinline__ void timeline_mark(uint32_t* c, int which) {
     if ((uint32_t)(threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))
@@ -320,7 +342,7 @@ __device__ __forceinline__ void timeline_mark(uint32_t* c, int which) {
 // bits) at its start, [1] closest hit done, [2] shading done, [3] end of its rays, [4] its end (after
 // the block epilogue); [5..8] the four trip counts; [9] HW_REG_XCC_ID; [10] HW_REG_HW_ID (CU, SIMD,
 // wave slot); [11] a tag (the tile, or the bounce kernel's 64-ray groups); [12] closest-hit traversal
-// start, [13] end of its prologue.  Stamps go to their own
+// start, [13] end of its prologue; [16..19] the RTK_TL_SPLIT words [8..11].  Stamps go to their own
 // buffer only; nothing the frame computes reads them.
 __device__ __forceinline__ void timeline_store(const Outputs& O, uint32_t w, uint32_t t0, uint32_t t1,
                                                const uint32_t* c, uint32_t tag) {
@@ -332,6 +354,7 @@ __device__ __forceinline__ void timeline_store(const Outputs& O, uint32_t w, uin
         r[2] = make_uint4(c[3], (uint32_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)),
                           (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)), tag);
         r[3] = make_uint4(c[6], c[7], 0u, 0u);
+        r[4] = make_uint4(c[8], c[9], c[10], c[11]);
     }
 }
 
@@ -994,6 +1017,9 @@ struct rt_ctx {
     } tline;
     bool frame_rows = false;   // rt_render_tiled: d_out is the whole frame (rtk::Outputs::frame_rows)
     uint32_t* h_stage = nullptr; size_t stage_cap = 0;   // rt_render_tiled: pinned frame for pageable callers
+    struct TiledWorker* worker = nullptr;   // rt_render_tiled: this context's host thread (ctxs[1..])
+    uint64_t enq_ns[2] = {0, 0};            // host steady clock at the start / end of the last frame's enqueue
+    double wait_ms = 0.0;                   // the last synchronous wait (wait_stream's spin cap)
     // rt_render's row groups: one stream (so one frame slot) per group, and the event they start after
     hipStream_t gstream[8] = {};
     hipEvent_t gstart = nullptr;
@@ -1009,7 +1035,8 @@ static std::string g_err;
 // is a fraction of a millisecond, so they poll instead (hipStreamQuery, RTAMD_SYNC=query, the
 // default) for up to kSpinWaitMs and only then block.  RTAMD_SYNC=block: hipStreamSynchronize
 // at once (A/B).
-constexpr double kSpinWaitMs = 50.0;
+constexpr double kSpinWaitMs = 50.0;    // cap of the spin
+constexpr double kSpinMinMs = 1.0;      // the spin lasts 4x the context's last wait, within [1, 50] ms
 static int sync_mode() {
     static const int m = [] {
         const char* v = std::getenv("RTAMD_SYNC");
@@ -1017,15 +1044,36 @@ static int sync_mode() {
     }();
     return m;
 }
-static hipError_t wait_stream(hipStream_t s) {
-    if (sync_mode() == 1) return hipStreamSynchronize(s);
+static inline void cpu_relax() { __builtin_ia32_pause(); }
+static uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// spin_ms: how long to poll before blocking (about the expected frame time: the caller passes a
+// multiple of its last wait); a pause between queries leaves the core's sibling and the memory
+// system alone
+static hipError_t wait_stream(hipStream_t s, double spin_ms = kSpinWaitMs, double* waited_ms = nullptr) {
     const auto t0 = std::chrono::steady_clock::now();
+    auto done = [&](hipError_t e) {
+        if (waited_ms) *waited_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return e;
+    };
+    if (sync_mode() == 1) return done(hipStreamSynchronize(s));
+    spin_ms = std::min(kSpinWaitMs, std::max(kSpinMinMs, spin_ms));
     for (;;) {
         const hipError_t e = hipStreamQuery(s);
-        if (e != hipErrorNotReady) return e;
-        if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > kSpinWaitMs)
-            return hipStreamSynchronize(s);
+        if (e != hipErrorNotReady) return done(e);
+        if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > spin_ms)
+            return done(hipStreamSynchronize(s));
+        for (int i = 0; i < 16; ++i) cpu_relax();
     }
+}
+// a context's synchronous wait: spins about 4x its previous wait, then blocks
+static hipError_t wait_ctx(rt_ctx* c, hipStream_t s) {
+    double ms = 0.0;
+    const hipError_t e = wait_stream(s, 4.0 * c->wait_ms, &ms);
+    c->wait_ms = ms;
+    return e;
 }
 
 // frame counters (one parity set): 8 per bounce ([0] queue size, [2] the bounce launch's
@@ -1362,8 +1410,10 @@ int rt_create(int device, rt_ctx** out) {
     return RT_OK;
 }
 
+static void tiled_worker_stop(rt_ctx* c);
 int rt_destroy(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID_ARG;
+    tiled_worker_stop(c);   // rt_render_tiled's host thread for this context, if it has one
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& f : c->slots)
@@ -1989,7 +2039,20 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
 
 int rt_render_device(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_tiling* tiling,
                      uint32_t* d_out, const rt_aux* d_aux, void* stream) {
-    return render_frames(c, w, h, depth, flags, tiling, d_out, d_aux, stream, nullptr, 1, 0);
+    const uint64_t t0 = now_ns();
+    const int rc = render_frames(c, w, h, depth, flags, tiling, d_out, d_aux, stream, nullptr, 1, 0);
+    if (c) {
+        c->enq_ns[0] = t0;
+        c->enq_ns[1] = now_ns();
+    }
+    return rc;
+}
+
+int rt_last_enqueue_time(rt_ctx* c, uint64_t* begin_ns, uint64_t* end_ns) {
+    if (!c || !begin_ns || !end_ns) return RT_ERR_INVALID_ARG;
+    *begin_ns = c->enq_ns[0];
+    *end_ns = c->enq_ns[1];
+    return RT_OK;
 }
 
 int rt_render_device_batch(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, const rt_tiling* tiling,
@@ -2013,7 +2076,7 @@ int rt_render_batch(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t f
         const int rc = render_frames(c, w, h, depth, flags, nullptr, (uint32_t*)pa.devicePointer, nullptr, c->stream,
                                      params, nframes, npix);
         if (rc) return rc;
-        HIPC(c, wait_stream(c->stream));
+        HIPC(c, wait_ctx(c, c->stream));
         return RT_OK;
     }
     (void)hipGetLastError();   // pageable memory: not an error, the read-back path below
@@ -2022,7 +2085,7 @@ int rt_render_batch(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t f
     if ((rc = render_frames(c, w, h, depth, flags, nullptr, c->d_out, nullptr, c->stream, params, nframes, npix)))
         return rc;
     HIPC(c, hipMemcpyAsync(out_bgr, c->d_out, npix * (size_t)nframes * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, wait_stream(c->stream));
+    HIPC(c, wait_ctx(c, c->stream));
     return RT_OK;
 }
 
@@ -2069,7 +2132,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
         if (hipPointerGetAttributes(&pa, out_bgr) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer) {
             rc = rt_render_device(c, w, h, depth, flags, nullptr, (uint32_t*)pa.devicePointer, nullptr, c->stream);
             if (rc) return rc;
-            HIPC(c, wait_stream(c->stream));
+            HIPC(c, wait_ctx(c, c->stream));
             return RT_OK;
         }
         (void)hipGetLastError();   // pageable memory: not an error, the readback path below
@@ -2087,7 +2150,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
             if (aux->t) HIPC(c, hipMemcpyAsync(aux->t, c->d_t, npix * depth * 4, hipMemcpyDeviceToHost, c->stream));
             if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb, c->d_rgb, npix * 3 * 4, hipMemcpyDeviceToHost, c->stream));
         }
-        HIPC(c, wait_stream(c->stream));
+        HIPC(c, wait_ctx(c, c->stream));
         return RT_OK;
     }
     for (uint32_t g = 0; g < groups; ++g)   // group g's kernels and readback on gstream[g]
@@ -2134,7 +2197,7 @@ int rt_render(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, 
             if (aux->rgb) HIPC(c, hipMemcpyAsync(aux->rgb + p0 * 3, c->d_rgb + p0 * 3, np * 3 * 4, hipMemcpyDeviceToHost, s));
         }
     }
-    for (uint32_t g = 0; g < groups; ++g) HIPC(c, wait_stream(c->gstream[g]));
+    for (uint32_t g = 0; g < groups; ++g) HIPC(c, wait_ctx(c, c->gstream[g]));
     c->last_group = slots;
     return RT_OK;
 }
@@ -2372,6 +2435,131 @@ int rt_scene_copy(rt_ctx* dst, rt_ctx* src) {
 constexpr int32_t kTiledBandRows = 8;
 constexpr int32_t kMaxTiled = 64;
 
+// One context's part of a tiled frame: its bands straight into the frame's rows (depth 1), or
+// into its band buffer and then one row-copy kernel; then the wait for its stream (also after a
+// failed enqueue: nothing may still write into the frame when rt_render_tiled returns).
+struct TiledJob {
+    uint32_t w, h;
+    int32_t depth;
+    uint32_t flags;
+    rt_tiling t;
+    uint32_t* frame;   // the frame as THIS context's device addresses it
+};
+static int tiled_enqueue(rt_ctx* c, const TiledJob& j) {
+    int rc = RT_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return set_err(c, "hipSetDevice failed", RT_ERR_DEVICE);
+    if (j.depth == 1) {   // the depth-1 kernel writes its pixels into the frame's rows itself
+        c->frame_rows = true;
+        rc = rt_render_device(c, j.w, j.h, j.depth, j.flags, &j.t, j.frame, nullptr, c->stream);
+        c->frame_rows = false;
+    } else {              // other kernels: the context's bands, then one row-copy kernel into the frame
+        const int64_t lp = rt_tiling_pixels(j.w, j.h, &j.t);
+        if (lp > 0 && (rc = ensure(c, c->d_out, c->out_cap, (size_t)lp)) == RT_OK &&
+            (rc = rt_render_device(c, j.w, j.h, j.depth, j.flags, &j.t, c->d_out, nullptr, c->stream)) == RT_OK &&
+            rt_bands_put(c->d_out, j.frame, j.w, j.h, &j.t, c->stream) != RT_OK)
+            rc = set_err(c, g_err, RT_ERR_DEVICE);
+    }
+    return rc;
+}
+static int tiled_wait(rt_ctx* c, int rc) {
+    const hipError_t e = hipSetDevice(c->device) == hipSuccess ? wait_ctx(c, c->stream) : hipErrorInvalidDevice;
+    if (e != hipSuccess && rc == RT_OK) rc = set_err(c, hipGetErrorString(e), RT_ERR_DEVICE);
+    return rc;
+}
+static int tiled_part(rt_ctx* c, const TiledJob& j) { return tiled_wait(c, tiled_enqueue(c, j)); }
+
+// rt_render_tiled's host thread per context (ctxs[1..n-1]; ctxs[0]'s part runs on the caller's
+// thread).  The hand-off is a sequence number the worker spins on, so all contexts enqueue at
+// once instead of one after another (~3-4 us of host time each): a condition
+// variable costs about as much as the enqueue it would save, so a worker spins for
+// kWorkerSpinMs after its last frame (a frame loop keeps it spinning) and only then sleeps.
+// RTAMD_TILED_WORKERS=0: every part on the caller's thread, one after another (A/B).
+constexpr double kWorkerSpinMs = 20.0;
+struct TiledWorker {
+    std::thread th;
+    std::atomic<uint64_t> posted{0}, finished{0};
+    std::atomic<bool> stop{false}, asleep{false};
+    std::mutex m;
+    std::condition_variable cv;
+    TiledJob job{};
+    int rc = RT_OK;
+};
+static void tiled_worker_loop(rt_ctx* c, TiledWorker* W) {
+    (void)hipSetDevice(c->device);
+    uint64_t seen = 0;
+    for (;;) {
+        auto t0 = std::chrono::steady_clock::now();
+        uint32_t spins = 0;
+        while (W->posted.load(std::memory_order_acquire) == seen && !W->stop.load(std::memory_order_relaxed)) {
+            cpu_relax();
+            if ((++spins & 4095u) == 0 &&
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > kWorkerSpinMs) {
+                std::unique_lock<std::mutex> lk(W->m);
+                W->asleep.store(true);   // seq_cst with the poster's store of `posted` then load of `asleep`
+                W->cv.wait(lk, [&] { return W->posted.load() != seen || W->stop.load(); });
+                W->asleep.store(false);
+                t0 = std::chrono::steady_clock::now();
+            }
+        }
+        if (W->stop.load()) return;
+        seen = W->posted.load(std::memory_order_acquire);
+        W->rc = tiled_part(c, W->job);
+        W->finished.store(seen, std::memory_order_release);
+    }
+}
+static void tiled_post(rt_ctx* c, const TiledJob& j) {
+    if (!c->worker) {
+        c->worker = new TiledWorker();
+        c->worker->th = std::thread(tiled_worker_loop, c, c->worker);
+    }
+    TiledWorker* W = c->worker;
+    W->job = j;
+    W->posted.fetch_add(1);   // seq_cst (the worker's asleep store / posted load pair)
+    if (W->asleep.load()) {
+        std::lock_guard<std::mutex> lk(W->m);
+        W->cv.notify_one();
+    }
+}
+static int tiled_join(rt_ctx* c) {
+    TiledWorker* W = c->worker;
+    const uint64_t want = W->posted.load();
+    while (W->finished.load(std::memory_order_acquire) != want) cpu_relax();
+    return W->rc;
+}
+static void tiled_worker_stop(rt_ctx* c) {
+    if (!c->worker) return;
+    {
+        std::lock_guard<std::mutex> lk(c->worker->m);
+        c->worker->stop.store(true);
+        c->worker->cv.notify_one();
+    }
+    if (c->worker->th.joinable()) c->worker->th.join();
+    delete c->worker;
+    c->worker = nullptr;
+}
+static bool tiled_workers_on() {
+    const char* v = std::getenv("RTAMD_TILED_WORKERS");
+    return !(v && std::strcmp(v, "0") == 0);
+}
+
+int32_t rt_tiled_direct_ok(int32_t n, const uint64_t* dev_addrs) {
+    if (n < 1 || !dev_addrs) return 0;
+    for (int32_t k = 0; k < n; ++k)
+        if (!dev_addrs[k] || (dev_addrs[k] & 15u)) return 0;   // unmapped on that device, or not 16-B aligned
+    return 1;
+}
+
+// rt_render_tiled: the frame is cut into 8-row bands dealt round-robin over the contexts
+// (rt_tiling).  Every context renders its bands on its own stream with the
+// frame-row output of the kernels (rtk::Outputs::frame_rows): each pixel store goes straight to
+// its place in ONE host frame, so every GPU sends its own rows over its own host link while it
+// renders, and there is no gather, copy or re-interleave step.  That frame is the caller's
+// buffer when every context's device can address it (hipHostGetDevicePointer on each device:
+// portable pinned memory, or memory registered and mapped for all of them), else ctxs[0]'s
+// portable pinned staging frame, copied to the caller's memory after the join.  Each context
+// addresses the frame through its own device's mapping.  ctxs[1..] enqueue and wait on their own
+// host threads (TiledWorker), ctxs[0] on the caller's; returns with the frame complete in out_bgr,
+// like raytrace_gpgpu (RayTracer.cpp:330-344).
 int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t depth, uint32_t flags, uint32_t* out_bgr) {
     if (!ctxs || n < 1 || n > kMaxTiled || !out_bgr || w == 0 || h == 0 || depth < 0 || depth > RT_MAX_DEPTH)
         return set_err(nullptr, "rt_render_tiled: invalid argument", RT_ERR_INVALID_ARG);
@@ -2389,16 +2577,17 @@ int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t de
             return set_err(c0, "rt_render_tiled: ctxs[" + std::to_string(k) + "] has no scene (rt_scene_copy)", RT_ERR_NO_SCENE);
     if (n == 1) return rt_render(c0, w, h, depth, flags, out_bgr, nullptr);
     const size_t npix = (size_t)w * h;
-    HIPC(c0, hipSetDevice(c0->device));
-    uint32_t* frame = nullptr;
-    bool staged = false;
-    hipPointerAttribute_t pa;
-    if (hipPointerGetAttributes(&pa, out_bgr) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer &&
-        !((uintptr_t)pa.devicePointer & 15u)) {   // (16-B aligned: the row-copy kernel's stores)
-        frame = (uint32_t*)pa.devicePointer;
-    } else {
-        staged = true;
-        (void)hipGetLastError();   // pageable memory: not an error
+    // the frame as every context's device addresses it: the caller's buffer if all of them map it
+    uint64_t addr[kMaxTiled] = {};
+    for (int32_t k = 0; k < n; ++k) {
+        void* dp = nullptr;
+        if (hipSetDevice(ctxs[k]->device) == hipSuccess && hipHostGetDevicePointer(&dp, out_bgr, 0) == hipSuccess)
+            addr[k] = (uint64_t)(uintptr_t)dp;
+    }
+    (void)hipGetLastError();   // pageable memory: not an error
+    const bool staged = !rt_tiled_direct_ok(n, addr);
+    if (staged) {
+        HIPC(c0, hipSetDevice(c0->device));
         if (c0->stage_cap < npix) {
             if (c0->h_stage) (void)hipHostFree(c0->h_stage);
             c0->h_stage = nullptr;
@@ -2406,42 +2595,47 @@ int rt_render_tiled(rt_ctx** ctxs, int32_t n, uint32_t w, uint32_t h, int32_t de
             HIPC(c0, hipHostMalloc((void**)&c0->h_stage, npix * 4, hipHostMallocPortable | hipHostMallocMapped));
             c0->stage_cap = npix;
         }
-        void* dp = nullptr;
-        HIPC(c0, hipHostGetDevicePointer(&dp, c0->h_stage, 0));
-        frame = (uint32_t*)dp;
-    }
-    int rc = RT_OK;
-    int32_t queued = 0;
-    for (; queued < n; ++queued) {
-        rt_ctx* c = ctxs[queued];
-        if (queued) {
-            c->params = c0->params;   // ctxs[0]'s camera drives the frame (updateCamera, RayTracer.cpp:671)
-            c->have_params = true;
-        }
-        const rt_tiling t{queued, n, kTiledBandRows, 0};
-        if (depth == 1) {   // the depth-1 kernel writes its pixels into the frame's rows itself
-            c->frame_rows = true;
-            rc = rt_render_device(c, w, h, depth, flags, &t, frame, nullptr, c->stream);
-            c->frame_rows = false;
-        } else {            // other kernels: the context's bands, then one row-copy kernel into the frame
-            const int64_t lp = rt_tiling_pixels(w, h, &t);
-            if (lp > 0 && (rc = ensure(c, c->d_out, c->out_cap, (size_t)lp)) == RT_OK &&
-                (rc = rt_render_device(c, w, h, depth, flags, &t, c->d_out, nullptr, c->stream)) == RT_OK &&
-                rt_bands_put(c->d_out, frame, w, h, &t, c->stream) != RT_OK)
-                rc = set_err(c, g_err, RT_ERR_DEVICE);
-        }
-        if (rc) {
-            if (c != c0) c0->err = "rt_render_tiled: ctxs[" + std::to_string(queued) + "]: " + c->err;
-            break;
+        for (int32_t k = 0; k < n; ++k) {
+            void* dp = nullptr;
+            HIPC(c0, hipSetDevice(ctxs[k]->device));
+            HIPC(c0, hipHostGetDevicePointer(&dp, c0->h_stage, 0));
+            addr[k] = (uint64_t)(uintptr_t)dp;
         }
     }
-    // join: every context that has work queued, also after a failure (nothing may still write
-    // into the frame when this returns)
-    for (int32_t k = 0; k < queued; ++k) {
+    const bool workers = tiled_workers_on();
+    int32_t posted = 0;
+    for (int32_t k = 1; k < n; ++k) {
         rt_ctx* c = ctxs[k];
-        const hipError_t e = hipSetDevice(c->device) == hipSuccess ? wait_stream(c->stream) : hipErrorInvalidDevice;
-        if (e != hipSuccess && rc == RT_OK)
-            rc = set_err(c0, "rt_render_tiled: ctxs[" + std::to_string(k) + "]: " + hipGetErrorString(e), RT_ERR_DEVICE);
+        c->params = c0->params;   // ctxs[0]'s camera drives the frame (updateCamera, RayTracer.cpp:671)
+        c->have_params = true;
+    }
+    if (workers)
+        for (; posted < n - 1; ++posted)
+            tiled_post(ctxs[posted + 1], TiledJob{w, h, depth, flags, rt_tiling{posted + 1, n, kTiledBandRows, 0},
+                                                  (uint32_t*)(uintptr_t)addr[posted + 1]});
+    int rc = RT_OK;
+    if (workers) {
+        rc = tiled_part(c0, TiledJob{w, h, depth, flags, rt_tiling{0, n, kTiledBandRows, 0}, (uint32_t*)(uintptr_t)addr[0]});
+    } else {   // every part enqueued on this thread, one after another, then every stream waited for
+        int rk[kMaxTiled];
+        for (int32_t k = 0; k < n; ++k)
+            rk[k] = tiled_enqueue(ctxs[k], TiledJob{w, h, depth, flags, rt_tiling{k, n, kTiledBandRows, 0},
+                                                    (uint32_t*)(uintptr_t)addr[k]});
+        for (int32_t k = 0; k < n; ++k) {
+            const int r = tiled_wait(ctxs[k], rk[k]);
+            if (r && rc == RT_OK) {
+                rc = r;
+                if (k) c0->err = "rt_render_tiled: ctxs[" + std::to_string(k) + "]: " + ctxs[k]->err;
+            }
+        }
+    }
+    // join every posted part, also after a failure (nothing may still write into the frame)
+    for (int32_t k = 1; k <= posted; ++k) {
+        const int r = tiled_join(ctxs[k]);
+        if (r && rc == RT_OK) {
+            rc = r;
+            c0->err = "rt_render_tiled: ctxs[" + std::to_string(k) + "]: " + ctxs[k]->err;
+        }
     }
     (void)hipSetDevice(c0->device);
     if (rc) return rc;
@@ -2509,6 +2703,8 @@ int rt_wave_timeline(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint32_t 
     words[1] = (uint32_t)frames;
     words[2] = (uint32_t)std::lround((double)t * 1e6);   // the first frame's kernels, HIP events, ns
     words[3] = (uint32_t)std::lround((double)k * 1e6);   // its first launch
+    words[4] = rtk::kTlRecord;                            // words per wave record
+    words[5] = RTK_TL_SPLIT;                              // memory-wait words stamped
     for (size_t i = 0; i < L; ++i) {
         words[8 + i] = c->tline.waves[i];
         words[40 + i] = c->tline.frame[i];

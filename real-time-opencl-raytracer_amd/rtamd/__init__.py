@@ -81,7 +81,8 @@ class rt_bvh_view(C.Structure):
 
 
 # every symbol include/rt_abi.h and include/rt_host.h declare
-ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_tiled", "rt_scene_copy",
+ABI_SYMBOLS = ["rt_create", "rt_upload_scene", "rt_set_params", "rt_render", "rt_render_tiled", "rt_tiled_direct_ok",
+               "rt_last_enqueue_time", "rt_scene_copy",
                "rt_render_device", "rt_render_device_batch", "rt_render_batch",
                "rt_tiling_pixels", "rt_assemble_bands", "rt_assemble_bands_batch", "rt_comm_unique_id", "rt_comm_create", "rt_comm_destroy",
                "rt_comm_last_error", "rt_frame_gather", "rt_frame_exchange", "rt_frame_slot_wait",
@@ -123,6 +124,8 @@ def lib() -> C.CDLL:
             "rt_render": (C.c_int, [vp, u32, u32, i32, u32, vp, C.POINTER(rt_aux)]),
             "rt_render_tiled": (C.c_int, [C.POINTER(vp), i32, u32, u32, i32, u32, vp]),
             "rt_scene_copy": (C.c_int, [vp, vp]),
+            "rt_tiled_direct_ok": (C.c_int32, [i32, C.POINTER(C.c_uint64)]),
+            "rt_last_enqueue_time": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
             "rt_render_device": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), vp, C.POINTER(rt_aux), vp]),
             "rt_render_device_batch": (C.c_int, [vp, u32, u32, i32, u32, C.POINTER(rt_tiling), C.POINTER(rt_params), i32,
                                                  vp, C.c_uint64, vp]),
@@ -511,11 +514,12 @@ class Renderer:
         _check(lib().rt_wave_timeline(self._h, w, h, depth, flags, frames, _ptr(buf), cap_words, C.byref(used)),
                self._h)
         nl = int(buf[0])
+        rw = int(buf[4]) or 16   # words per wave record (16 before the memory-wait words)
         recs, off = [], 128
         for k in range(nl):
             nw = int(buf[8 + k])
-            recs.append((int(buf[40 + k]), int(buf[72 + k]), buf[off:off + nw * 16].reshape(nw, 16).copy()))
-            off += nw * 16
+            recs.append((int(buf[40 + k]), int(buf[72 + k]), buf[off:off + nw * rw].reshape(nw, rw).copy()))
+            off += nw * rw
         base = min(int(r[:, 0].min()) for _, _, r in recs) if recs else 0
         out = []
         for fr, bo, r in recs:
@@ -527,7 +531,11 @@ class Renderer:
                         "main_c": a[:, 5], "pro_c": a[:, 6], "main_s": a[:, 7], "pro_s": a[:, 8],
                         "xcc": a[:, 9] & 0xF, "hwid": a[:, 10], "tag": a[:, 11], "t_enter": a[:, 12],
                         "t_pro_end": a[:, 13]})
-        return {"frame_ns": int(buf[2]), "first_ns": int(buf[3]), "frames": int(buf[1]), "launches": out}
+            if rw >= 20:   # RTK_TL_SPLIT builds: main-loop memory wait (ticks) and long-wait trips
+                out[-1].update({"wait_c": a[:, 16], "wait_s": a[:, 17], "longwait_c": a[:, 18],
+                                "longwait_s": a[:, 19]})
+        return {"frame_ns": int(buf[2]), "first_ns": int(buf[3]), "frames": int(buf[1]), "launches": out,
+                "split": bool(buf[5])}
 
     def copy_scene_from(self, src: "Renderer") -> None:
         """rt_scene_copy: this ctx gets src's uploaded scene (device to device / peer to peer)."""
@@ -651,6 +659,12 @@ class Renderer:
         _check(lib().rt_last_deferred(self._h, C.byref(v)), self._h)
         return v.value
 
+    def last_enqueue_time(self):
+        """rt_last_enqueue_time: host steady-clock ns at the start / end of the last frame's enqueue."""
+        b, e = C.c_uint64(), C.c_uint64()
+        _check(lib().rt_last_enqueue_time(self._h, C.byref(b), C.byref(e)), self._h)
+        return b.value, e.value
+
     def overflow_count(self) -> int:
         v = C.c_uint64()
         _check(lib().rt_overflow_count(self._h, C.byref(v)), self._h)
@@ -672,6 +686,13 @@ def render_tiled(renderers, w: int, h: int, depth: int = 3, flags: int = 0, out=
     if rc:
         _check(rc, renderers[0]._h if n else None)
     return None if isinstance(out, int) else out
+
+
+def tiled_direct_ok(dev_addrs) -> bool:
+    """rt_tiled_direct_ok: whether rt_render_tiled writes the caller's buffer directly, given the
+    device address each context's device resolved for it (0 = unmapped on that device)."""
+    a = (C.c_uint64 * max(1, len(dev_addrs)))(*dev_addrs)
+    return bool(lib().rt_tiled_direct_ok(len(dev_addrs), a))
 
 
 def tiling_pixels(w: int, h: int, rank: int, nranks: int, band_rows: int) -> int:

@@ -78,7 +78,7 @@ def main():
         else:
             t = d[1 + wf: 1 + wf + j["steps"]]
         timed_us = round(sum(t) / len(t), 2) if t else None
-        hip_ms = j["roofline"]["kernel_ms"]
+        hip_ms = j["roofline"].get("kernel_ms_per_launch", j["roofline"].get("kernel_ms"))
     fetch, nf, ff = counter("prof_fetch", "FETCH_SIZE")
     write, nw, fw = counter("prof_write", "WRITE_SIZE")
     shutil.copy(ff, os.path.join(out, f"{cfg}_pmc_fetch.csv"))

@@ -96,3 +96,20 @@ def test_multi_gpu_and_diagnostic_entry_points_reject_bad_arguments_without_gpu(
     assert lib.rt_wave_timeline(None, 8, 8, 1, 0, 1, po, 256, C.byref(used)) == -1
     ms, waves = C.c_float(), C.c_uint64()
     assert lib.rt_chase_latency(None, 16, 4, 4, 1, C.byref(ms), C.byref(waves)) == -1
+    assert lib.rt_last_enqueue_time(None, C.byref(waves), C.byref(waves)) == -1
+
+
+def test_tiled_frame_direct_or_staged_per_device():
+    """rt_render_tiled writes the caller's buffer directly only when EVERY context's device resolved
+    a device address for it (hipHostGetDevicePointer on that device) and each is 16-B aligned (the
+    row-copy kernel's stores); one device that cannot map it, or a misaligned mapping, sends the
+    whole frame through the portable pinned staging frame."""
+    ok = rtamd.tiled_direct_ok
+    base = 0x7F0000000000
+    assert ok([base])
+    assert ok([base + 16 * k for k in range(8)])                 # 8 devices, each its own mapping
+    assert not ok([base, base, 0, base])                          # device 2 cannot address it
+    assert not ok([0] * 8)                                        # pageable memory
+    assert not ok([base, base + 4])                               # a mapping not 16-B aligned
+    assert not ok([])
+    assert rtamd.lib().rt_tiled_direct_ok(2, None) == 0

@@ -123,14 +123,22 @@ def test_a_late_rank_at_set_up(barrier):
         assert "torch.distributed gather" in cfg["band_exchange"]
 
 
-def test_frame_check_catches_a_band_from_another_frame():
+@pytest.mark.parametrize("steps,fpl", [(10, None), (40, 1)])
+def test_frame_check_catches_a_band_from_another_frame(steps, fpl):
     """The last rank puts frame 4's bands from another frame's buffer: the per-frame checksum
-    (orbiting camera: every frame differs) must flag exactly that frame."""
-    p = _ranks_on_one_gpu(2, ["--steps", "10", "--orbit", "0.01", "--frame-check", "every",
-                              "--inject-fault", "wrong-bands"])
+    (orbiting camera: every frame differs) must flag exactly that frame.  With 40 steps at one
+    frame per launch the bad frame's buffer has been overwritten by the end (8 frames held), so
+    only the checksum can fail the run."""
+    extra = ["--steps", str(steps), "--orbit", "0.01", "--frame-check", "every", "--inject-fault", "wrong-bands"]
+    if fpl:
+        extra += ["--frames-per-launch", str(fpl)]
+    p = _ranks_on_one_gpu(2, extra)
     assert p.returncode == 0, _why(p)
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert res["config"]["frame_check"]["checksum_mismatches"] == 1
+    fc = res["config"]["frame_check"]
+    assert fc["checksum_mismatches"] == 1 and fc["mismatched_frames"] == [4], fc
+    if steps == 40:
+        assert "held_frames_differing" not in fc, fc
     assert res["config"]["gathered_frame_equals_single_rank_render"] is False
 
 
