@@ -83,6 +83,12 @@
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
 #endif
+#ifndef RTK_PRIO_TRIPS
+#define RTK_PRIO_TRIPS 0    // A/B: > 0: a wave past this many main-loop trips raises its issue priority
+#endif
+#ifndef RTK_XFRAME
+#define RTK_XFRAME 0        // A/B: a batch launch's bounce queues tile-major, frame-minor (first_bounce_batch_kernel)
+#endif
 #ifndef RTK_LEAFRUN
 #define RTK_LEAFRUN 0       // A/B: a wave past RTK_LEAFRUN_TRIPS main-loop trips tests a leaf's remaining
 #endif                      // triangles in one trip (the long waves that set a frame's latency)
@@ -810,25 +816,33 @@ __device__ __forceinline__ void set_status(uint32_t* sync, uint32_t code) {
 }
 
 // rt_bands_put_sync: at most kPutBlocks blocks, each copying every gridDim.x-th local row.
-// Before writing set `set` for its use `use` each block waits until rank 0 has presented the
-// set's previous use (back-pressure: a peer never overwrites a frame rank 0 has not yet observed
-// complete).  The grid is capped so that puts waiting on their sets hold few CU slots: a waiting
-// put with a block per row (1,080 at one rank) could fill a GPU shared by several ranks and starve
-// the very renders its wait depends on until the bound expires.  After its rows, every block
+// Before writing set `set` for its use `use` the put waits until rank 0 has presented the set's
+// previous use (back-pressure: a peer never overwrites a frame rank 0 has not yet observed
+// complete).  By default that wait is the queue's (qwait: hipStreamWaitValue32 on the release
+// word, enqueued before this kernel), so a waiting put holds no CU slot at all and cannot starve
+// the renders its wait depends on (round 5: puts spinning on the GPU, a block per row, filled a
+// GPU shared by three ranks); the kernel then only checks the status word.  Without it
+// (RTAMD_PUT_WAIT=kernel, or a device without stream wait values) each block's first lane spins,
+// bounded by timeout_ticks, and the grid is capped so that waiting puts hold few CU slots.  A
+// present that times out poisons every release word (kReleasePoison) after setting the status,
+// so puts waiting in their queues go on, see the status and write nothing.  After its rows, every block
 // releases its stores at system scope (each XCD's L2 written back) and counts itself on this
 // rank's own counter for the set; the block that completes the count publishes
 // arrive[set][rank] = use + 1 with a system-scope release store.
 constexpr uint32_t kPutBlocks = 64;
+constexpr uint32_t kReleasePoison = 0x7FFFFFFFu;   // >= every use, signed or unsigned compare
 __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restrict__ frame,
                                                              const uint32_t* __restrict__ bands, uint32_t w,
                                                              uint32_t local_rows, uint32_t rank, uint32_t nranks,
                                                              uint32_t band_rows, uint32_t* sync, uint32_t* local,
                                                              uint32_t nsets, uint32_t set, uint32_t use,
-                                                             uint64_t timeout_ticks) {
+                                                             uint64_t timeout_ticks, uint32_t qwait) {
     __shared__ uint32_t s_abort;
     if (threadIdx.x == 0) {
         uint32_t ab = 0;
-        if (use > 0) {
+        if (qwait) {
+            ab = sys_load(sync) != 0u ? 1u : 0u;   // the queue waited; a failed exchange writes nothing
+        } else if (use > 0) {
             const uint64_t t0 = now_ticks();
             while (sys_load(sync + kSyncHead + set) < use) {
                 // once any wait has failed (status != 0) the exchange is over: no further wait
@@ -885,11 +899,14 @@ __global__ void __launch_bounds__(64) frame_present_kernel(uint32_t* sync, uint3
         }
     }
     const bool all_ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+    if (!all_ok) {
+        if (lane == 0) set_status(sync, 2u);
+        // every put waiting in a queue for a set's release goes on (and, seeing the status, writes nothing)
+        for (uint32_t s2 = lane; s2 < nsets; s2 += 64)
+            __hip_atomic_store(sync + kSyncHead + s2, kReleasePoison, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     if (lane == 0) {
-        if (!all_ok) {
-            set_status(sync, 2u);
-            return;
-        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (release) __hip_atomic_store(sync + kSyncHead + set, use + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -898,7 +915,7 @@ __global__ void __launch_bounds__(64) frame_present_kernel(uint32_t* sync, uint3
 
 // rt_frame_release: rank 0 is done with use `use` of set `set`; the ranks may refill it.
 __global__ void __launch_bounds__(64) frame_release_kernel(uint32_t* sync, uint32_t set, uint32_t use) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && sys_load(sync) == 0u) {   // after a failure the sets stay poisoned (released for good)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // the frame's readers are done (stream order)
         __hip_atomic_store(sync + kSyncHead + set, use + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1320,6 +1337,19 @@ int64_t rt_frame_sync_words(int32_t nsets, int32_t nranks) {
     return (int64_t)rtk::kSyncHead + nsets + (int64_t)nsets * nranks;
 }
 
+// rt_bands_put_sync's wait for a set's release: in the queue (hipStreamWaitValue32, default) where
+// the current device supports stream wait values, else in the kernel (RTAMD_PUT_WAIT=kernel forces it)
+static bool put_queue_wait() {
+    const char* v = std::getenv("RTAMD_PUT_WAIT");
+    if (v && std::strcmp(v, "kernel") == 0) return false;
+    int dev = 0, ok = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return ok != 0;
+}
 static uint64_t timeout_ticks(uint32_t ms) { return (uint64_t)(ms ? ms : 10000u) * 100000ull; }   // s_memrealtime: 100 MHz
 
 int rt_bands_put_sync(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, uint32_t h, const rt_tiling* tiling,
@@ -1337,10 +1367,17 @@ int rt_bands_put_sync(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, ui
         return set_err(nullptr, "rt_bands_put_sync: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
     const uint32_t local_rows = (uint32_t)(npix / w);
     (void)hipGetLastError();   // an earlier call's error is not this launch's
+    const bool qwait = put_queue_wait();
+    if (qwait && use > 0) {   // the queue waits for the set's release (no CU slot held while waiting)
+        const hipError_t we = hipStreamWaitValue32((hipStream_t)stream, d_sync + rtk::kSyncHead + set, use,
+                                                   hipStreamWaitValueGte, 0xFFFFFFFFu);
+        if (we != hipSuccess) return set_err(nullptr, std::string("rt_bands_put_sync: hipStreamWaitValue32: ") +
+                                                          hipGetErrorString(we), RT_ERR_DEVICE);
+    }
     hipLaunchKernelGGL(rtk::bands_put_sync_kernel, dim3(std::min<uint32_t>(local_rows, rtk::kPutBlocks)), dim3(256), 0,
                        (hipStream_t)stream, d_frame, d_bands,
                        w, local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows, d_sync, d_local,
-                       (uint32_t)nsets, (uint32_t)set, use, timeout_ticks(timeout_ms));
+                       (uint32_t)nsets, (uint32_t)set, use, timeout_ticks(timeout_ms), qwait ? 1u : 0u);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(nullptr, std::string("rt_bands_put_sync: ") + hipGetErrorString(e), RT_ERR_DEVICE);
     return RT_OK;
