@@ -48,7 +48,7 @@ def parse_args(argv=None):
     ap.add_argument("--orbit", type=float, default=0.0,
                     help="moving camera: add_rotate(ORBIT, 0) radians per frame, as the reference's mouse "
                          "drag does (RayTracer.cpp:553-565); 0 = the static default camera")
-    ap.add_argument("--jitter", type=int, default=16,
+    ap.add_argument("--jitter", type=int, default=32,
                     help="static camera: cycle through this many sub-pixel jittered copies of it (frame n: camera "
                          "n %% J, the image plane shifted by a Halton(2,3) offset inside one pixel; camera 0 is the "
                          "unjittered one), so no two frames of a launch or of the frames in flight trace the same "
@@ -207,9 +207,22 @@ def jittered_cameras(p, w, h, n):
     return out
 
 
+_SYNC = []   # the run's rtamd.FrameSync (ipc exchange), for the failure report
+
+
+def _sync_state():
+    if not _SYNC:
+        return "none (no IPC exchange set up)"
+    try:
+        st, presented = _SYNC[0].status()
+        return f"status {st} (0 ok, 1 a put timed out, 2 a present timed out), {presented} frames presented"
+    except Exception as e:   # the device may be the thing that failed
+        return f"unreadable ({e})"
+
+
 def _hang_exit(rank, seconds):
-    print(f"bench.py: rank {rank} still running {seconds:.0f} s after joining the process group; exiting",
-          file=sys.stderr, flush=True)
+    print(f"bench.py: rank {rank} still running {seconds:.0f} s after joining the process group; exiting; "
+          f"frame-sync block: {_sync_state()}", file=sys.stderr, flush=True)
     os._exit(3)
 
 
@@ -233,7 +246,15 @@ def main():
     result_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
-    run(args, world, result_out)
+    try:
+        run(args, world, result_out)
+    except BaseException as e:
+        # every failed rank says so on its own stderr, with the frame-sync block as it stands (the
+        # round-4 3-rank abort left only the launcher's summary: DESIGN.md 8); then the failure goes on
+        if not (isinstance(e, SystemExit) and e.code in (0, None)):
+            print(f"bench.py: rank {os.environ.get('RANK', '0')} failed: {type(e).__name__}: {e}; "
+                  f"frame-sync block: {_sync_state()}", file=sys.stderr, flush=True)
+        raise
 
 
 def run(args, world, result_out=None):
@@ -405,14 +426,14 @@ def run(args, world, result_out=None):
     B = max(1, args.gather_batch) if ((use_dist and not ipc) or args.local_batch) else 1
     # default frames per launch (profiles/r05/ab/frames_per_launch_ab.log): depth 1: 4 (C3 0.298 ms at 4,
     # 0.300 at 8); the wavefront mode: 8 (C5 0.796 ms at 8, 0.802 at 4, 0.838 at 1)
-    # (a wavefront batch needs contiguous frames: every rank's pixels a whole slot, decided alike on every rank)
-    wf_batch = depth > 1 and bool(flags & 8) and all(
-        rtamd.tiling_pixels(w, h, q, shard_n, args.band_rows) == cap for q in range(shard_n))
+    # (a wavefront batch's frames sit `cap` pixels apart in the rank's buffers, every rank alike: a rank
+    # with fewer bands than rank 0 keeps the slot size; since round 6 the batch takes such a stride)
+    wf_batch = depth > 1 and bool(flags & 8)
     FPL = args.frames_per_launch if args.frames_per_launch > 0 else (4 if depth == 1 else 8 if wf_batch else 1)
     if FPL > 1:   # a batch = the frames of one rt_render_device_batch launch (and of one gather at N > 1)
         if depth < 1 or (depth > 1 and not wf_batch) or FPL > rtamd.RT_MAX_BATCH:
-            raise SystemExit(f"bench.py: --frames-per-launch needs depth 1 or the wavefront mode (with contiguous "
-                             f"frames at depth > 1) and K <= {rtamd.RT_MAX_BATCH}")
+            raise SystemExit(f"bench.py: --frames-per-launch needs depth 1 or the wavefront mode "
+                             f"and K <= {rtamd.RT_MAX_BATCH}")
         B = FPL
     # buffer sets: batch i uses set i % NB.  At N > 1 the sets cycle 2F ways, so a batch never
     # renders into a set whose gather was issued less than F batches earlier: the gathers run
@@ -453,6 +474,7 @@ def run(args, world, result_out=None):
         """Every rank leaves the IPC band puts for the torch.distributed gather (B stays 1)."""
         nonlocal ipc, tgather, shared, shm, fsync, frames, gbufs, glists
         ipc, tgather, fsync = False, True, None
+        _SYNC.clear()
         if shared is not None:
             shared.close()
             shared = None
@@ -508,6 +530,7 @@ def run(args, world, result_out=None):
             sync_local = torch.zeros(NQ, dtype=torch.int32, device=dev)   # this rank's per-set block counters
             fsync = rtamd.FrameSync(w, h, tiling, shard_n, NQ, fr_base + 4 * nfr_words, sync_local.data_ptr(),
                                     args.sync_timeout_ms)
+            _SYNC[:] = [fsync]
             if args.shard:   # the N-1 shards no process puts: their arrivals never hold the present up
                 a0 = nfr_words + sync_words - NQ * shard_n   # arrive[set][rank] ends the block
                 arrive = torch.full((NQ, shard_n), -1, dtype=torch.int32, device=dev)   # 0xFFFFFFFF >= every use

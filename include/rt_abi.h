@@ -210,9 +210,8 @@ int rt_render_device(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_
  * server -- gets the longest tiles of all of them scheduled first in one grid instead of on
  * separate streams.  depth 1 (primary + shadow ray, RT_FLAG_NO_SHADOW for primary
  * only), or depth > 1 with RT_FLAG_WAVEFRONT: bounce 0 of every frame in one launch, then each
- * bounce launch over all frames' ray queues; such a batch needs contiguous frames (frame_stride =
- * the rank's pixels) and one light position for all frames (the reference's light is a global,
- * RayTracer.cpp:60).  No aux planes; every frame's pixels equal rt_render_device's for its camera.
+ * bounce launch over all frames' ray queues; such a batch needs one light position for all frames
+ * (the reference's light is a global, RayTracer.cpp:60).  No aux planes; every frame's pixels equal rt_render_device's for its camera.
  * Asynchronous like rt_render_device; rt_last_timing is the launch (all nframes frames).
  * The ctx's own params (rt_set_params) are neither read nor changed. */
 int rt_render_device_batch(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,

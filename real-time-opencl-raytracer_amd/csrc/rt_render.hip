@@ -87,7 +87,7 @@
 #define RTK_PRIO_TRIPS 0    // A/B: > 0: a wave past this many main-loop trips raises its issue priority
 #endif
 #ifndef RTK_XFRAME
-#define RTK_XFRAME 0        // A/B: a batch launch's bounce queues tile-major, frame-minor (first_bounce_batch_kernel)
+#define RTK_XFRAME 1        // a batch launch's bounce queues tile-major, frame-minor (first_bounce_batch_kernel; 0: frame-major)
 #endif
 #ifndef RTK_LEAFRUN
 #define RTK_LEAFRUN 0       // A/B: a wave past RTK_LEAFRUN_TRIPS main-loop trips tests a leaf's remaining
@@ -1784,10 +1784,12 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     if (npix < 0) return set_err(c, "rt_render_device: bad tiling", RT_ERR_INVALID_ARG);
     if (batch && bstride < (uint64_t)npix)
         return set_err(c, "rt_render_device_batch: frame_stride below the frame's pixels", RT_ERR_INVALID_ARG);
-    if (batch && depth > 1 && bstride != (uint64_t)npix)
-        return set_err(c, "rt_render_device_batch: depth > 1 needs contiguous frames (frame_stride = the frame's pixels)",
-                       RT_ERR_INVALID_ARG);
-    if (batch && (uint64_t)npix * K >= (1ull << 32))
+    // a batch launch's pixel space: frame f's pixel p is f * fpx + p -- the global traversal stack
+    // is indexed in it, and at depth > 1 so are the rays the bounce launches carry, which finish
+    // at out[f * fpx + p]: there fpx is the frame stride (frames need not be contiguous: a rank's
+    // band buffers padded to the largest rank's, bench.py at N > 1), at depth 1 the frame's pixels
+    const uint64_t fpx = batch && depth > 1 ? bstride : (uint64_t)npix;
+    if (batch && fpx * K >= (1ull << 32))
         return set_err(c, "rt_render_device_batch: more than 2^32 pixels in one launch", RT_ERR_INVALID_ARG);
     if (batch && d_aux) return set_err(c, "rt_render_device_batch: no aux planes", RT_ERR_INVALID_ARG);
     const bool aux = d_aux && d_aux->hits && d_aux->t && d_aux->rgb;
@@ -1846,7 +1848,7 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     O.t = aux ? d_aux->t : nullptr;
     O.rgb = aux ? d_aux->rgb : nullptr;
     O.overflow = c->d_overflow;
-    O.local_pixels = (uint64_t)npix * K;   // a batch launch's pixel space: its frames one after the other
+    O.local_pixels = fpx * K;   // a batch launch's pixel space: its frames one after the other
     O.fcount = nullptr;
     O.frame_rows = c->frame_rows && !batch ? 1u : 0u;
     O.wtime = nullptr;
@@ -1871,7 +1873,7 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
     // the fused kernel specialised to a single bounce
     const bool wavefront = ((flags & RT_FLAG_WAVEFRONT) && depth > 0) || depth == 1;
 
-    if ((rc = ensure(c, L.d_gstack, L.gstack_cap, (size_t)npix * rtk::kGlobalStack * K))) return rc;
+    if ((rc = ensure(c, L.d_gstack, L.gstack_cap, (size_t)fpx * rtk::kGlobalStack * K))) return rc;
     O.gstack = L.d_gstack;
     // frame counters, two parity sets: per bounce k (kBounceWords from kBounceWords k) its
     // queue size and its work cursor; [kRestartSlot] restarted traversals; then per queue
@@ -2018,7 +2020,7 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
                                              make_float4(Q.light_pos.x, Q.light_pos.y, Q.light_pos.z, 0.0f)};
                 }
                 C.stride = bstride;
-                C.frame_px = (uint32_t)npix;
+                C.frame_px = (uint32_t)fpx;
                 void* bargs[] = {&S, &F, &O, &W, &C};
                 void* kb = kernel_batch(math, fast, depth > 1);
                 if (ext_ev) HIPC(c, hipExtLaunchKernel(kb, grid, block, bargs, 0, s, E.e[0], E.e[1], 0));

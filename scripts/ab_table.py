@@ -11,7 +11,10 @@ from collections import defaultdict
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ab"
 rows = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(d, "*.json"))):
-    v, c, r = os.path.basename(f)[:-5].rsplit("_", 2)
+    parts = os.path.basename(f)[:-5].rsplit("_", 2)
+    if len(parts) == 2:
+        parts.append("1")
+    v, c, r = parts
     try:
         j = json.load(open(f))
     except ValueError:
