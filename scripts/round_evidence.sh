@@ -19,9 +19,11 @@ trace1() {   # trace1 CONFIG: kernel trace + stats at one frame in flight
 }
 export -f trace1
 export rnd
-scripts/gpu_steps.sh \
-  "pytest_gpu|420|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" \
-  "smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
+# SKIP_TESTS=1: the profile, traces and bench lines only (the suite and smoke in a call of their own)
+tests=("pytest_gpu|900|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread"
+       "smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'")
+[ -n "$SKIP_TESTS" ] && tests=()
+scripts/gpu_steps.sh "${tests[@]}" \
   "profile|600|scripts/profile_c3.sh && PMC_SETS=occ scripts/pmc_configs.sh gpurun_out/$rnd/pmc_occ c3 && python scripts/profile_summary.py $rnd c3 --occupancy gpurun_out/$rnd/pmc_occ && mkdir -p gpurun_out/profiles_$rnd && cp profiles/$rnd/c3_* profiles/$rnd/pmc_c3.json gpurun_out/profiles_$rnd/" \
   "trace1_c3|150|trace1 c3" "trace1_c4|200|trace1 c4" "trace1_c5|300|trace1 c5" \
   "bench_c3|240|python bench.py" \

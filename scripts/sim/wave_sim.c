@@ -71,6 +71,9 @@ static void cull_top(lane* L) {
     }
 }
 static long long deep_lanes = 0;   // lanes whose stack outgrew the LDS part (the product restarts them)
+static int HELP = 0, HELP_G = 4;   // env HELP=L: with <= L live lanes, a lane in a leaf tests up to HELP_G of
+                                  // its triangles per iteration (idle lanes of the wave testing them for it)
+static long long helped_extra = 0;
 static int T2 = 0, TT2 = 0;   // TT2=1: two triangles of one leaf per iteration   // env T2=1: an inner step that descends into an inner child runs that child's step too
 static int descended;  // set by lane_step: this inner step moved cur to a child (push or advance)
 static void lane_step(lane* L) {
@@ -162,8 +165,17 @@ static void run_wave(lane* L, int* act) {
             ld_row += !sr;
             ld_both += !sq && !sr;
         }
+        int live = 0;
+        for (int i = 0; i < 64; ++i) live += act[i] && L[i].sc > 0;
+        const int help = HELP && live <= HELP;
         for (int i = 0; i < 64; ++i) if (act[i] && L[i].sc > 0) {
+            const int leaf0 = L[i].stack[L[i].sc - 1];
+            const int in_leaf = N[leaf0].l < 0;
             lane_step(&L[i]); lane_steps++;
+            if (help && in_leaf)
+                for (int k = 1; k < HELP_G && L[i].sc > 0 && L[i].stack[L[i].sc - 1] == leaf0 && L[i].tk < L[i].tend; ++k) {
+                    lane_step(&L[i]); helped_extra++;
+                }
             if (T2 && descended && L[i].sc > 0 && N[L[i].stack[L[i].sc - 1]].l >= 0) { lane_step(&L[i]); t2_second++; }
             else if (TT2 && rec[i] < 0 && L[i].sc > 0 && N[L[i].stack[L[i].sc - 1]].l < 0 && L[i].tk < L[i].tend &&
                      lane_record(&L[i]) == rec[i] - 1) { lane_step(&L[i]); t2_second++; }   // the leaf's next triangle
@@ -176,6 +188,8 @@ int main(int argc, char** argv) {
     T2 = getenv("T2") ? atoi(getenv("T2")) : 0;
     TT2 = getenv("TT2") ? atoi(getenv("TT2")) : 0;
     CULL = getenv("CULL") ? atoi(getenv("CULL")) : 0;
+    HELP = getenv("HELP") ? atoi(getenv("HELP")) : 0;
+    HELP_G = getenv("HELP_G") ? atoi(getenv("HELP_G")) : 4;
     size_t s;
     N = (node*)rd("c3_nodes.bin", &s); NN = (int)(s / sizeof(node));
     V = (float*)rd("c3_vertices.bin", 0); IDX = (int32_t*)rd("c3_indices.bin", 0); REF = (int32_t*)rd("c3_tri_indices.bin", 0);
@@ -234,6 +248,7 @@ int main(int argc, char** argv) {
            (double)lane_steps / (64.0 * (double)(iters + iters_pro)));
     if (T2 || TT2) printf("T2: second inner steps taken without a fetch: %lld\n", t2_second);
     if (CULL) printf("CULL=%d: popped inner entries skipped %lld\n", CULL, culled);
+    if (HELP) printf("HELP=%d (groups of %d): triangle tests taken by helper lanes %lld\n", HELP, HELP_G, helped_extra);
     printf("rays whose stack outgrew 16 LDS entries: %lld\n", deep_lanes);
     printf("iters %lld prologue %lld  lane fetches(vec) %lld  quad req %lld (inner %lld tri %lld) lanes/qreq %.3f\n",
            iters, iters_pro, lanes_vec, q_vec, q_vec_inner, q_vec_tri, (double)lanes_vec / q_vec);

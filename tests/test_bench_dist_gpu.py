@@ -97,6 +97,23 @@ def test_bench_ranks_sharing_the_gpu_assemble_the_frame(n, fpl):
     print(f"{n} ranks: set-up skew {res['config']['setup_skew_s']} s")
 
 
+def test_ranks_sharing_the_gpu_wavefront_batches_with_ragged_bands():
+    """C5 (10 M tris, depth 3 wavefront, 8 frames per launch) on 2 ranks: 1080p has 135 8-row
+    bands, so rank 1 holds one band fewer than rank 0 and its batch launches take frames a slot
+    (rank 0's pixel count) apart -- the round-6 strided wavefront batch, with the bounce queues in
+    the cross-frame order.  Every frame of an orbiting camera is checksummed when rank 0 sees it
+    complete and compared with rank 0's own one-rank render."""
+    p = _ranks_on_one_gpu(2, ["--config", "c5", "--steps", "16", "--orbit", "0.01", "--frame-check", "every",
+                              "--hang-timeout", "250"],
+                          timeout=280)
+    assert p.returncode == 0, _why(p)
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = res["config"]
+    assert cfg["frames_per_launch"] == 8 and cfg["depth"] == 3
+    assert cfg["frame_delivery"]["status"] == 0 and cfg["frame_check"]["checksum_mismatches"] == 0, cfg["frame_check"]
+    assert cfg["gathered_frame_equals_single_rank_render"] is True
+
+
 @pytest.mark.parametrize("barrier", [True, False])
 def test_a_late_rank_at_set_up(barrier):
     """The round-4 abort's set-up hypothesis, made deterministic: the last of 3 ranks
