@@ -33,4 +33,5 @@ scripts/gpu_steps.sh "${tests[@]}" \
   "bench_c4|240|python bench.py --config c4 --no-cpu-baseline" \
   "bench_c5|300|python bench.py --config c5 --no-cpu-baseline" \
   "bench_c5u|300|python bench.py --config c5u --no-cpu-baseline" \
-  "bench_orbit|240|python bench.py --orbit 0.002 --no-cpu-baseline"
+  "bench_orbit|240|python bench.py --orbit 0.002 --no-cpu-baseline" \
+  "bench_c3_static|240|python bench.py --jitter 1 --no-cpu-baseline"
