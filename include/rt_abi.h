@@ -309,9 +309,9 @@ int rt_peer_access(int32_t device, int32_t peer, int32_t* can);
  * times a set has been filled (0, 1, 2, ...).  Per frame:
  *   every rank: rt_bands_put_sync(..., d_sync, d_local, nsets, set, use, timeout, stream) --
  *     first waits until rank 0 has presented the set's previous use (no rank ever overwrites
- *     a frame rank 0 has not observed complete) -- in the queue (hipStreamWaitValue32 on the
- *     set's release word, so a waiting put holds no CU slot; RTAMD_PUT_WAIT=kernel, or a device
- *     without stream wait values: a bounded spin in the kernel) --, then copies its rows (as rt_bands_put), then
+ *     a frame rank 0 has not observed complete) -- one wave of its own waits, bounded, before the
+ *     put's blocks start (RTAMD_PUT_WAIT=stream: hipStreamWaitValue32 instead, which ROCm runs as
+ *     its own polling blit kernel without a bound; =kernel: every put block waits) --, then copies its rows (as rt_bands_put), then
  *     publishes "use done" for this rank with a system-scope release; d_local = nsets uint32
  *     counters in the rank's own memory, zeroed once;
  *   rank 0, after its own put: rt_frame_present(d_sync, nsets, set, use, nranks, timeout,
@@ -320,9 +320,8 @@ int rt_peer_access(int32_t device, int32_t peer, int32_t* can);
  *     the complete frame.  With release != 0 it also hands the set back to the ranks for its
  *     next use; otherwise rank 0 calls rt_frame_release(d_sync, nsets, set, use, stream)
  *     after the frame's consumers (a display copy, a checksum) on that stream.
- * rank 0's waits are bounded (timeout_ms, 0 = 10 s); a timeout sets a status instead of hanging
- * and releases every set (a put waiting in its queue then goes on and writes nothing; a put
- * waiting in the kernel is bounded by timeout_ms itself):
+ * Waits are bounded (timeout_ms, 0 = 10 s); a timeout sets a status instead of hanging, and a
+ * present that times out also releases every set (waits in flight end; their puts write nothing):
  * rt_frame_sync_status reads it (0 ok, 1 a put timed out, 2 a present timed out) and the
  * number of frames presented (synchronous).  rt_frame_checksum adds a position-dependent
  * 64-bit sum of a frame's pixels into *d_sum (frame checks). */

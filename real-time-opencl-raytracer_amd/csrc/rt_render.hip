@@ -818,15 +818,17 @@ __device__ __forceinline__ void set_status(uint32_t* sync, uint32_t code) {
 // rt_bands_put_sync: at most kPutBlocks blocks, each copying every gridDim.x-th local row.
 // Before writing set `set` for its use `use` the put waits until rank 0 has presented the set's
 // previous use (back-pressure: a peer never overwrites a frame rank 0 has not yet observed
-// complete).  By default that wait is the queue's (qwait: hipStreamWaitValue32 on the release
-// word, enqueued before this kernel), so a waiting put holds no CU slot at all and cannot starve
-// the renders its wait depends on (round 5: puts spinning on the GPU, a block per row, filled a
-// GPU shared by three ranks); the kernel then only checks the status word.  Without it
-// (RTAMD_PUT_WAIT=kernel, or a device without stream wait values) each block's first lane spins,
-// bounded by timeout_ticks, and the grid is capped so that waiting puts hold few CU slots.  A
-// present that times out poisons every release word (kReleasePoison) after setting the status,
-// so puts waiting in their queues go on, see the status and write nothing.  After its rows, every block
-// releases its stores at system scope (each XCD's L2 written back) and counts itself on this
+// complete).  Round 5 found that wait starving a GPU shared by three ranks: every block of every
+// waiting put spun, holding its CU slot, while the renders the wait depended on queued behind
+// them.  Now (prewaited, the default, RTAMD_PUT_WAIT=wave) the wait is ONE wave of its own
+// (put_wait_kernel, bounded by timeout_ticks, status 1 on expiry) enqueued before the put, and the
+// put's blocks only check the status word.  RTAMD_PUT_WAIT=stream enqueues hipStreamWaitValue32
+// instead -- on device memory that is not HSA signal memory ROCm runs that as its own polling blit
+// kernel (__amd_rocclr_streamOpsWait, one per wait in a kernel trace, profiles/r06/qwait_trace/),
+// i.e. the same single polling wave but without a bound; RTAMD_PUT_WAIT=kernel: every put block
+// waits (round 5).  A present that times out poisons every release word (kReleasePoison) after
+// setting the status, so waits in flight end and their puts, seeing the status, write nothing.
+// After its rows, every block releases its stores at system scope (each XCD's L2 written back) and counts itself on this
 // rank's own counter for the set; the block that completes the count publishes
 // arrive[set][rank] = use + 1 with a system-scope release store.
 constexpr uint32_t kPutBlocks = 64;
@@ -836,12 +838,12 @@ __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restric
                                                              uint32_t local_rows, uint32_t rank, uint32_t nranks,
                                                              uint32_t band_rows, uint32_t* sync, uint32_t* local,
                                                              uint32_t nsets, uint32_t set, uint32_t use,
-                                                             uint64_t timeout_ticks, uint32_t qwait) {
+                                                             uint64_t timeout_ticks, uint32_t prewaited) {
     __shared__ uint32_t s_abort;
     if (threadIdx.x == 0) {
         uint32_t ab = 0;
-        if (qwait) {
-            ab = sys_load(sync) != 0u ? 1u : 0u;   // the queue waited; a failed exchange writes nothing
+        if (prewaited) {
+            ab = sys_load(sync) != 0u ? 1u : 0u;   // waited for before this launch; a failed exchange writes nothing
         } else if (use > 0) {
             const uint64_t t0 = now_ticks();
             while (sys_load(sync + kSyncHead + set) < use) {
@@ -880,6 +882,21 @@ __global__ void __launch_bounds__(256) bands_put_sync_kernel(uint32_t* __restric
             __hip_atomic_store(sync + kSyncHead + nsets + set * nranks + rank, use + 1u, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
+    }
+}
+
+// rt_bands_put_sync's wait for set `set`'s release (the default mode): one wave, its first lane
+// polling, bounded; on expiry status 1 (the put that follows then writes nothing)
+__global__ void __launch_bounds__(64) put_wait_kernel(uint32_t* sync, uint32_t set, uint32_t use, uint64_t timeout_ticks) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = now_ticks();
+    while (sys_load(sync + kSyncHead + set) < use) {
+        if (sys_load(sync) != 0u) return;   // the exchange has already failed
+        if (now_ticks() - t0 > timeout_ticks) {
+            set_status(sync, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(8);
     }
 }
 
@@ -1337,18 +1354,21 @@ int64_t rt_frame_sync_words(int32_t nsets, int32_t nranks) {
     return (int64_t)rtk::kSyncHead + nsets + (int64_t)nsets * nranks;
 }
 
-// rt_bands_put_sync's wait for a set's release: in the queue (hipStreamWaitValue32, default) where
-// the current device supports stream wait values, else in the kernel (RTAMD_PUT_WAIT=kernel forces it)
-static bool put_queue_wait() {
+// rt_bands_put_sync's wait for a set's release (RTAMD_PUT_WAIT): 0 = one bounded wait wave before the
+// put (default, "wave"), 1 = hipStreamWaitValue32 ("stream", where the device supports stream wait
+// values), 2 = every put block waits ("kernel", round 5)
+static int put_wait_mode() {
     const char* v = std::getenv("RTAMD_PUT_WAIT");
-    if (v && std::strcmp(v, "kernel") == 0) return false;
-    int dev = 0, ok = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess) {
+    if (v && std::strcmp(v, "kernel") == 0) return 2;
+    if (v && std::strcmp(v, "stream") == 0) {
+        int dev = 0, ok = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && ok)
+            return 1;
         (void)hipGetLastError();
-        return false;
+        return 2;
     }
-    return ok != 0;
+    return 0;
 }
 static uint64_t timeout_ticks(uint32_t ms) { return (uint64_t)(ms ? ms : 10000u) * 100000ull; }   // s_memrealtime: 100 MHz
 
@@ -1367,13 +1387,17 @@ int rt_bands_put_sync(const uint32_t* d_bands, uint32_t* d_frame, uint32_t w, ui
         return set_err(nullptr, "rt_bands_put_sync: buffers must be 16-byte aligned", RT_ERR_INVALID_ARG);
     const uint32_t local_rows = (uint32_t)(npix / w);
     (void)hipGetLastError();   // an earlier call's error is not this launch's
-    const bool qwait = put_queue_wait();
-    if (qwait && use > 0) {   // the queue waits for the set's release (no CU slot held while waiting)
+    const int mode = put_wait_mode();
+    if (mode == 0 && use > 0) {   // one wave waits for the set's release; the put's blocks do not
+        hipLaunchKernelGGL(rtk::put_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_sync, (uint32_t)set, use,
+                           timeout_ticks(timeout_ms));
+    } else if (mode == 1 && use > 0) {
         const hipError_t we = hipStreamWaitValue32((hipStream_t)stream, d_sync + rtk::kSyncHead + set, use,
                                                    hipStreamWaitValueGte, 0xFFFFFFFFu);
         if (we != hipSuccess) return set_err(nullptr, std::string("rt_bands_put_sync: hipStreamWaitValue32: ") +
                                                           hipGetErrorString(we), RT_ERR_DEVICE);
     }
+    const bool qwait = mode != 2;
     hipLaunchKernelGGL(rtk::bands_put_sync_kernel, dim3(std::min<uint32_t>(local_rows, rtk::kPutBlocks)), dim3(256), 0,
                        (hipStream_t)stream, d_frame, d_bands,
                        w, local_rows, (uint32_t)T->rank, (uint32_t)T->nranks, (uint32_t)T->band_rows, d_sync, d_local,

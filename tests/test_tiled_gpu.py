@@ -56,6 +56,43 @@ def test_tiled_fixture_frames_equal_rt_render(renderer, n):
         _close(rs)
 
 
+@pytest.mark.parametrize("workers", ["1", "0"])
+def test_tiled_workers_and_caller_thread_agree(renderer, monkeypatch, workers):
+    """ctxs[1..] on their own host threads (the default) or all enqueued by the caller in turn
+    (RTAMD_TILED_WORKERS=0): the same frame as rt_render, frame after frame with the camera
+    moving, the workers' threads reused across calls; every context's launch is stamped
+    (rt_last_enqueue_time) within this call."""
+    import time
+    import rtamd
+    monkeypatch.setenv("RTAMD_TILED_WORKERS", workers)
+    d = load_golden("knot16k")
+    scene = rtamd.Scene.from_arrays(d)
+    renderer.upload(scene)
+    rs = _renderers(4)
+    try:
+        rs[0].upload(scene)
+        for r in rs[1:]:
+            r.copy_scene_from(rs[0])
+        w, h = 160, 96
+        cam = rtamd.Camera()
+        mesh = rtamd.Mesh.torus_knot(128, 64)
+        for i in range(12):
+            cam.add_rotate(0.05, 0.0)
+            p = cam.params(mesh, w, h)
+            renderer.set_params(p)
+            rs[0].set_params(p)
+            depth = 1 if i % 3 else 3
+            want = renderer.render(w, h, depth=depth, flags=0)
+            t0 = time.monotonic_ns()
+            got = rtamd.render_tiled(rs, w, h, depth, 0)
+            t1 = time.monotonic_ns()
+            assert np.array_equal(got, want), (workers, i, int(np.sum(got != want)))
+            stamps = [r.last_enqueue_time() for r in rs]
+            assert all(t0 <= b <= e <= t1 for b, e in stamps), (stamps, t0, t1)
+    finally:
+        _close(rs)
+
+
 def test_tiled_argument_and_scene_errors(renderer):
     import rtamd
     d = load_golden("knot16k")
