@@ -201,7 +201,9 @@ int rt_scene_copy(rt_ctx* dst, rt_ctx* src);
 int rt_render_device(rt_ctx* ctx, uint32_t w, uint32_t h, int32_t depth, uint32_t flags,
                      const rt_tiling* tiling, uint32_t* d_out, const rt_aux* d_aux, void* stream);
 
+#ifndef RT_MAX_BATCH
 #define RT_MAX_BATCH 8
+#endif
 /* Throughput mode of rt_render_device: nframes (1..RT_MAX_BATCH) frames of one size, frame i
  * with camera params[i] (updateCamera's Params, RayTracer.cpp:609-672; every params[i] must
  * carry the same scene box), rendered by ONE launch into d_out + i * frame_stride (pixels,

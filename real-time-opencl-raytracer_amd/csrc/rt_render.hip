@@ -61,8 +61,10 @@
 #define RTK_WFB_REF_WAVES 8 // waves per SIMD the S_ref bounce kernel is bounded to
 #endif
 #ifndef RTK_WF_GRID_PCT
-#define RTK_WF_GRID_PCT 75  // persistent bounce grid, percent of the blocks the chip holds at once
-                            // (C5 0.838 vs 0.849 ms at 100 %, profiles/r04/ab/grid_8waves_ab.log)
+#define RTK_WF_GRID_PCT 50  // persistent bounce grid, percent of the blocks the chip holds at once (C5 with
+                            // 8 frames per launch: 38 / 44 / 50 / 56 / 62 / 68 / 75 % -> 0.758 / 0.752 / 0.750 / 0.753 /
+                            // 0.755 / 0.760 / 0.757 ms, one frame per launch 0.827 vs 0.836 at 75 %, one frame alone
+                            // 1.28 vs 1.25: profiles/r06/ab/c5_grid_pct_ab*.txt; round 4 at one frame per launch: 75 %)
 #endif
 #ifndef RTK_FB_WAVES
 #define RTK_FB_WAVES 8      // waves per SIMD the S_ref depth-1 kernel is bounded to

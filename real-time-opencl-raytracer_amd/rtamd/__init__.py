@@ -35,7 +35,7 @@ RT_FLAG_WAVEFRONT = 8
 RT_FLAG_WF_SORT = 32
 RT_FLAG_STRICT_MATH = 64
 RT_MAX_DEPTH = 8
-RT_MAX_BATCH = 8   # rt_render_device_batch frames per launch
+RT_MAX_BATCH = int(os.environ.get("RTAMD_MAX_BATCH", "8"))   # rt_render_device_batch frames per launch (RTAMD_MAX_BATCH: an A/B build's)
 ERRORS = {0: "RT_OK", -1: "RT_ERR_INVALID_ARG", -2: "RT_ERR_DEVICE", -3: "RT_ERR_NO_SCENE",
           -4: "RT_ERR_OUT_OF_MEMORY", -5: "RT_ERR_BAD_SCENE"}
 
