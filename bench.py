@@ -424,7 +424,7 @@ def run(args, world, result_out=None):
     # once per B frames
     # (ipc: a frame's put is one copy issued right after its render, no batching)
     B = max(1, args.gather_batch) if ((use_dist and not ipc) or args.local_batch) else 1
-    # default frames per launch (profiles/r05/ab/frames_per_launch_ab.log): depth 1: 4 (C3 0.298 ms at 4,
+    # default frames per launch (profiles/archive/r05.tar.gz: r05/ab/frames_per_launch_ab.log): depth 1: 4 (C3 0.298 ms at 4,
     # 0.300 at 8); the wavefront mode: 8 (C5 0.796 ms at 8, 0.802 at 4, 0.838 at 1)
     # (a wavefront batch's frames sit `cap` pixels apart in the rank's buffers, every rank alike: a rank
     # with fewer bands than rank 0 keeps the slot size; since round 6 the batch takes such a stride)
