@@ -156,7 +156,11 @@ struct QRay {
 // segments) sum, from which wf_compact_sort_kernel's blocks find where their chunk starts
 // in the bounce's dense order `perm` (compacted, optionally sorted), with no scan launch.
 #ifndef RTK_SORT_SCALE
-#define RTK_SORT_SCALE 4    // bounce sort: 2 x this many direction buckets over [-1, 1] (at most 8)
+#define RTK_SORT_SCALE 4    // bounce sort: 2 x this many direction buckets over [-1, 1], one frame per launch
+#endif
+#ifndef RTK_SORT_SCALE_BATCH
+#define RTK_SORT_SCALE_BATCH 8   // the same for launches of >= 4 frames (a chunk holds one tile of every frame, RTK_XFRAME:
+                                 // C5 0.744 vs 0.753 ms with 8 buckets; one frame per launch loses with 16: profiles/r06/ab/)
 #endif
 #ifndef RTK_CHUNK_SEGS
 #define RTK_CHUNK_SEGS 32   // segments per sort chunk (C5: 16 -> 0.900 ms, 32 -> 0.881, 64 -> 0.900; profiles/r04/ab/sort_chunk_ab.log)
@@ -613,7 +617,7 @@ __device__ void tile_epilogue(const Frame& F, uint32_t tb, uint32_t t_start, uin
 // Stable: inside a bucket the rays keep their slot order, so neighbouring pixels (a quad's
 // four rays, appended side by side) stay side by side and keep sharing their record fetches.
 // Slot j = c0 + 256 p + t is ranked among the entries of its bucket by (pass p, wave, lane):
-// peers in a wave by a 3-bit ballot match, earlier waves and passes by LDS counts.
+// peers in a wave by a ballot match on the key's bits, earlier waves and passes by LDS counts.
 // The block of the queue's last segment stores the queue's size in *total.  nseg is
 // `nseg_fixed` (bounce 1: the first bounce's waves), or when 0 the previous bounce's 64-ray
 // groups, ceil(*prev_total / 64).
@@ -624,9 +628,11 @@ __global__ void __launch_bounds__(256) wf_compact_sort_kernel(const QRay* __rest
                                                               const uint32_t* __restrict__ super_sum, uint32_t nseg_fixed,
                                                               const uint32_t* __restrict__ prev_total,
                                                               uint32_t* __restrict__ total_out, uint32_t* __restrict__ perm,
-                                                              uint32_t axis, uint32_t sort) {
+                                                              uint32_t axis, uint32_t sort) {   // sort: 0, or the key's scale
     constexpr uint32_t kPasses = kLocalSortChunk / 256;
-    constexpr uint32_t kBuckets = 8;
+    constexpr uint32_t kBuckets = 2 * (RTK_SORT_SCALE > RTK_SORT_SCALE_BATCH ? RTK_SORT_SCALE : RTK_SORT_SCALE_BATCH);
+    constexpr int kKeyBits = kBuckets <= 2 ? 1 : kBuckets <= 4 ? 2 : kBuckets <= 8 ? 3 : kBuckets <= 16 ? 4 : 5;
+    static_assert((kBuckets & (kBuckets - 1)) == 0 && kBuckets <= 32, "the key's buckets: a power of two, <= 32");
     __shared__ uint32_t cnt[kBuckets][kPasses * 4];   // [bucket][pass * 4 + wave]: entries, then their offsets
     __shared__ uint32_t total[kBuckets];
     __shared__ uint32_t segc[kChunkSegs];
@@ -658,11 +664,11 @@ __global__ void __launch_bounds__(256) wf_compact_sort_kernel(const QRay* __rest
         if (valid && sort) {
             const float4 b = q[j].b;   // {d.xyz, shadow sum}
             const float d = axis == 0 ? b.x : axis == 1 ? b.y : b.z;
-            k = d == d ? (uint32_t)min(max((int)((d + 1.0f) * (float)RTK_SORT_SCALE), 0), 2 * RTK_SORT_SCALE - 1) : 0u;
+            k = d == d ? (uint32_t)min(max((int)((d + 1.0f) * (float)sort), 0), 2 * (int)sort - 1) : 0u;
         }
         uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
-        for (int bit = 0; bit < 3; ++bit) {
+        for (int bit = 0; bit < kKeyBits; ++bit) {
             const uint64_t m = __builtin_amdgcn_ballot_w64((k >> bit) & 1u);
             peers &= ((k >> bit) & 1u) ? m : ~m;
         }
@@ -2075,7 +2081,8 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
             hipLaunchKernelGGL(rtk::wf_compact_sort_kernel, dim3((uint32_t)nchunk), dim3(256), 0, s,
                                (const rtk::QRay*)qbuf(k), (const uint32_t*)L.d_seg, (const uint32_t*)sums(k),
                                (const uint32_t*)(sums(k) + nchunk), k == 1 ? (uint32_t)nseg : 0u,
-                               (const uint32_t*)(bc - kBounceWords), bc, L.d_perm, thin, sort ? 1u : 0u);
+                               (const uint32_t*)(bc - kBounceWords), bc, L.d_perm, thin,
+                               sort ? (K >= 4 ? (uint32_t)RTK_SORT_SCALE_BATCH : (uint32_t)RTK_SORT_SCALE) : 0u);
             W.perm = L.d_perm;
             W.out = k + 1 < depth ? qbuf(k + 1) : nullptr;
             W.seg_cnt = L.d_seg;
