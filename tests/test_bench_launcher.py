@@ -41,3 +41,27 @@ def test_world_size_must_match_gpus():
     p = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--probe-launch"], capture_output=True, text=True,
                        timeout=60, env=_env(WORLD_SIZE="2", RANK="0"), cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=2" in p.stderr
+
+
+def test_jittered_cameras_are_distinct_subpixel_shifts():
+    """bench.py's default cameras: copy 0 is the camera itself, every copy differs from every other,
+    and each moves the image plane by less than half a pixel along a and b (volumeRender.cl:1169-1190:
+    image_pos = c + a xf + b yf, xf = (x - 0.5) / w), with the eye, light and scene box unchanged."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    rng = np.random.default_rng(7)
+    p = rng.normal(size=32).astype(np.float32) * 100
+    w, h = 1920, 1080
+    cams = bench.jittered_cameras(p, w, h, 32)
+    assert cams.shape == (32, 32) and np.array_equal(cams[0], p)
+    assert len({c.tobytes() for c in cams}) == 32
+    a, b = p[0:3].astype(np.float64), p[4:7].astype(np.float64)
+    A = np.stack([a, b], 1)
+    for c in cams[1:]:
+        d = c[8:11].astype(np.float64) - p[8:11].astype(np.float64)
+        (dx, dy), *_ = np.linalg.lstsq(A, d, rcond=None)
+        assert abs(dx * w) <= 0.5 + 1e-3 and abs(dy * h) <= 0.5 + 1e-3, (dx * w, dy * h)
+        mask = np.ones(32, bool)
+        mask[8:11] = False
+        assert np.array_equal(c[mask], p[mask])
