@@ -638,10 +638,10 @@ def run(args, world, result_out=None):
         fr_ptr = [f.data_ptr() for f in frames] if rank == 0 else [0] * NB
         # (--shard: the one-rank communicator assembles this rank's own bands only)
         slot_wait, xchg = comms[0].frame_exchanger(cap, w, cap // w if args.shard else h, args.band_rows)
-    pg = gopts = g_out = g_in = assemble = frame_ptr = gbuf_ptr = asm_stream = asm_sh = asm_done = None
+    pg = gopts = g_out = g_in = assemble = frame_ptr = gbuf_ptr = asm_stream = asm_sh = asm_done = gathered = None
 
     def torch_gather_state():
-        nonlocal pg, gopts, g_out, g_in, assemble, frame_ptr, gbuf_ptr, asm_stream, asm_sh, asm_done
+        nonlocal pg, gopts, g_out, g_in, assemble, frame_ptr, gbuf_ptr, asm_stream, asm_sh, asm_done, gathered
         pg = dist.distributed_c10d._get_default_group()
         gopts = dist.GatherOptions()
         gopts.rootRank = 0
@@ -655,6 +655,7 @@ def run(args, world, result_out=None):
             asm_stream = torch.cuda.Stream(dev)
             asm_sh = asm_stream.cuda_stream
             asm_done = [torch.cuda.Event() for _ in range(NB)]
+            gathered = [torch.cuda.Event() for _ in range(NB)]
     if tgather:
         torch_gather_state()
 
@@ -692,7 +693,13 @@ def run(args, world, result_out=None):
         work = pg.gather(g_out[j], g_in[j], gopts)
         pending[j] = work
         if rank == 0:
+            # the assembly after the gather: work.wait() orders it after the collective's own stream,
+            # and the event after whatever the gather enqueued on the current stream (a one-rank group
+            # may copy there instead: with distinct frames every frame, the assembly then read the set's
+            # previous contents 1 run in 6 -- profiles/r06/repro_dist_check/)
+            gathered[j].record(streams[k])
             torch.cuda.set_stream(asm_stream)
+            asm_stream.wait_event(gathered[j])
             work.wait()   # the assembly stream after the gather
             assemble(frame_ptr[j], gbuf_ptr[j], asm_sh, nfr)
             asm_done[j].record(asm_stream)
