@@ -85,17 +85,8 @@
 #ifndef RTK_LDS_STACK
 #define RTK_LDS_STACK 16    // LDS part of the traversal stack (C3 peaks at 9; deeper rays restart)
 #endif
-#ifndef RTK_PRIO_TRIPS
-#define RTK_PRIO_TRIPS 0    // A/B: > 0: a wave past this many main-loop trips raises its issue priority
-#endif
 #ifndef RTK_XFRAME
 #define RTK_XFRAME 1        // a batch launch's bounce queues tile-major, frame-minor (first_bounce_batch_kernel; 0: frame-major)
-#endif
-#ifndef RTK_LEAFRUN
-#define RTK_LEAFRUN 0       // A/B: a wave past RTK_LEAFRUN_TRIPS main-loop trips tests a leaf's remaining
-#endif                      // triangles in one trip (the long waves that set a frame's latency)
-#ifndef RTK_LEAFRUN_TRIPS
-#define RTK_LEAFRUN_TRIPS 64
 #endif
 
 namespace rtk {
