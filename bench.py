@@ -960,6 +960,7 @@ def run(args, world, result_out=None):
             lat.append((time.perf_counter() - t1) * 1e3)
         lat = sorted(lat[1:])
         frame_latency = {"ms_per_frame_median": round(lat[len(lat) // 2], 4), "ms_per_frame_min": round(lat[0], 4),
+                         "ms_per_frame_mean": round(sum(lat) / len(lat), 4), "ms_per_frame_max": round(lat[-1], 4),
                          "frames": len(lat), "how": "one frame at a time: launch + device synchronize, host clock"}
         if orbit_params is not None:
             set_params(hdl, orbit_params[0])

@@ -91,8 +91,9 @@ enum {
     RT_FLAG_EXACT_DIV = 4u,  /* force the division form of the slab test (volumeRender.cl:614-615) instead
                                 of the bit-identical fast quotient; for A/B only */
     RT_FLAG_STATIC_ORDER = 16u /* keep the static XCD-dealt block order instead of the adaptive
-                                longest-first order built from the previous frame's per-block times
-                                (DESIGN.md 6.2); pixels are identical either way */
+                                longest-first order built from the per-block times of the context's
+                                latest rebuild launch on the stream slot (every 8th launch;
+                                RTAMD_LPT_EVERY); pixels are identical either way */
 };
 
 #define RT_MAX_DEPTH 8       /* reference: RAY_TRACE_DEPTH 3 (volumeRender.cl:12) */

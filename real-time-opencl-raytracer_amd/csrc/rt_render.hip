@@ -1356,6 +1356,23 @@ int64_t rt_frame_sync_words(int32_t nsets, int32_t nranks) {
 // rt_bands_put_sync's wait for a set's release (RTAMD_PUT_WAIT): 0 = one bounded wait wave before the
 // put (default, "wave"), 1 = hipStreamWaitValue32 ("stream", where the device supports stream wait
 // values), 2 = every put block waits ("kernel", round 5)
+// Launches per rebuild of the adaptive longest-first block order (RTAMD_LPT_EVERY=K, K >= 1;
+// default 8).  A rebuild launch times its blocks (each block's epilogue: a barrier, its cost
+// store and a counter round trip) and its last block sorts them; every other launch runs the
+// order as it is and has no epilogue at all, so a wave that is done leaves at once.  Against a
+// rebuild every launch (K = 1): C2 0.0605 vs 0.0693 ms per frame, one frame alone 0.172 vs 0.239
+// ms; C3 0.2988 vs 0.3028, one frame 0.364 vs 0.372; C4 1.0765 vs 1.089; the orbiting camera
+// 0.280 vs 0.283 (K = 16 lets its order go stale: one frame's mean 0.376 vs 0.373 at K = 8);
+// profiles/r06/ab_lpt_every/table.txt.  The order is a schedule, never a pixel: same frames.
+static uint64_t lpt_every() {
+    static const uint64_t k = [] {
+        const char* v = std::getenv("RTAMD_LPT_EVERY");
+        const long n = v ? std::atol(v) : 8L;
+        return (uint64_t)(n >= 1 ? n : 1);
+    }();
+    return k;
+}
+
 static int put_wait_mode() {
     const char* v = std::getenv("RTAMD_PUT_WAIT");
     if (v && std::strcmp(v, "kernel") == 0) return 2;
@@ -1970,9 +1987,14 @@ static int render_frames(rt_ctx* c, uint32_t w, uint32_t h, int32_t depth, uint3
             L.cost_ready = false;
         }
         if (L.cost_ready) F.tile_order = L.d_lpt;
-        F.tile_cost = L.d_cost;
-        F.lpt_next = L.d_lpt;
-        F.done = L.d_done;
+        // The order is rebuilt every lpt_every()-th launch on the slot (and whenever it is not
+        // ready): only those launches time their blocks, and their last block sorts; the others
+        // run the order as it is, with no epilogue at all (a wave that is done leaves at once).
+        if (!L.cost_ready || L.nframe % lpt_every() == 0) {
+            F.tile_cost = L.d_cost;
+            F.lpt_next = L.d_lpt;
+            F.done = L.d_done;
+        }
     }
     // the fast kernels (any quotient domain: traverse_fast picks the variant) need a clean scene
     // whose records one buffer descriptor covers
