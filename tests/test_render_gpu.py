@@ -679,11 +679,12 @@ def test_render_readback_paths_agree(renderer):
                                              (640, 360, 3, WAVEFRONT | WF_SORT)])
 def test_adaptive_order_renders_every_tile_of_a_moving_camera(renderer, w, h, depth, flags):
     """Frames of an orbiting camera rendered one after another on one stream each use the
-    longest-first block order the previous frame's last block built (rtk::tile_epilogue: costs
-    read 16 per thread per round trip, bucket keys kept in LDS up to kKeyBytes blocks, re-read
-    beyond: 3840x2160 has 32,400 blocks).  Every frame starts from a sentinel-filled buffer and
-    must equal the static-order render of its camera: an order that is not a permutation of the
-    blocks leaves sentinel pixels (a skipped tile) behind."""
+    longest-first block order built by the stream slot's latest rebuild launch (launches 0, 8
+    and 16 here: the order is rebuilt every 8th launch, the launches between have no block
+    epilogue; rtk::tile_epilogue: costs read 16 per thread per round trip, bucket keys kept in
+    LDS up to kKeyBytes blocks, re-read beyond: 3840x2160 has 32,400 blocks).  Every frame starts
+    from a sentinel-filled buffer and must equal the static-order render of its camera: an order
+    that is not a permutation of the blocks leaves sentinel pixels (a skipped tile) behind."""
     import torch
     import rtamd
     d = load_golden("knot16k")
@@ -692,7 +693,7 @@ def test_adaptive_order_renders_every_tile_of_a_moving_camera(renderer, w, h, de
     cam = rtamd.Camera()
     buf = torch.empty(w * h, dtype=torch.int32, device="cuda")
     s = torch.cuda.Stream()
-    for f in range(5):
+    for f in range(18):
         cam.add_rotate(0.07, 0.0)
         renderer.set_params(rtamd.params_to_array(cam.params(m, w, h)))
         with torch.cuda.stream(s):
