@@ -385,7 +385,8 @@ int rt_chase_latency(rt_ctx* ctx, uint32_t table_records, uint32_t iters, uint32
  * bounce (0 = the first launch); from word 128, 16 words per wave, launch after launch, waves in
  * blockIdx * 4 + wave order: s_memrealtime (100 MHz, low 32 bits) at the wave's start, when its
  * closest-hit traversal returned, when its shading was done, at the end of its rays and at its
- * end (after the block epilogue: the longest-first order build in the frame's last block); its
+ * end (after the block epilogue of a launch that rebuilds the longest-first order, every 8th on
+ * a stream slot: the order build in its last block; other launches have no epilogue); its
  * closest-hit main-loop and wave-uniform-prologue trips and the same two for its shadow rays;
  * HW_REG_XCC_ID; HW_REG_HW_ID; the tile it rendered (first launch) or the 64-ray groups it took
  * (bounce launches; trips summed over them, times of the last); s_memrealtime when the closest-hit
