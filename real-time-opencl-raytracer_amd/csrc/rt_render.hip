@@ -327,8 +327,8 @@ __device__ __forceinline__ uint32_t frame_row(const Frame& F, uint32_t lr) {
 // inner_step's box test as n <= min(f, tHit) && f >= kTmin (1, default) instead of three compares
 // and two mask ANDs (0): same result for every input (rt_kernel_body.inc); the main loop issues two
 // SALU instructions fewer per trip.  C2 0.0587 vs 0.0603 ms per frame, C3 0.2914 vs 0.2978, C4
-// 1.046 vs 1.073 (three runs each, profiles/r06/ab_imin/table.txt); 2 (the bound as a NaN-sentinel
-// select) makes the loop 10 instructions longer
+// 1.046 vs 1.073 (three runs each, profiles/r06/ab_imin/table.txt); the bound as a NaN-sentinel
+// select instead (folding f >= kTmin in as well) made the loop 10 instructions longer
 #ifndef RTK_IMIN
 #define RTK_IMIN 1
 #endif
